@@ -1,0 +1,172 @@
+/*
+ * libldgpu -- MI355X (gfx950) LaserDisc RF -> .tbc decode: public C ABI.
+ *
+ * Plain C, plain pointers and sizes; no C++ or torch types cross this boundary.
+ * Every entry point returns an int status (LDG_OK == 0) and never throws.
+ *
+ * The ABI is the seam a drop-in replaces in the reference ld-decode snapshot:
+ *
+ *   reference seam (file:line)                          replaced by
+ *   ---------------------------------------------------  --------------------------------
+ *   loader plugin  loader(infile, sample, readlen)      ldg_set_capture (GPU unpack of
+ *     lddutils.py:117-229, set lddecode.py:53-58          u8 / s16 / .r30 / .lds)
+ *   RFDecode(system) filter build                       ldg_create + ldg_set_filters
+ *     lddecode_core.py:119-279
+ *   RFDecode.demod(infile, start, 1e6, mtf)             ldg_decode_reads (demod part)
+ *     lddecode_core.py:373-427
+ *   FieldNTSC/FieldPAL(rf, rawdecode, 0, ...)           ldg_decode_reads (field part):
+ *     lddecode_core.py:889-1191                            per read -> ldg_field_info +
+ *                                                          device-resident dspicture
+ *   Field.downscale(audio) -> downscale_audio           ldg_field_audio
+ *     lddecode_core.py:431-484, 809-810
+ *   Framer.formatoutput(fields)                         ldg_assemble_frames
+ *     lddecode_core.py:1238-1252
+ *   comb-ntsc stdin/stdout frame stream, dim=2          ldg_comb_ntsc
+ *     comb-ntsc.cxx:834-892, 1099-1117
+ *
+ * The Python host (ld-decode_amd/ldgpu) keeps readfield/readframe/mergevbi,
+ * the read-position / MTF / audio-offset chains and the file writers, and
+ * calls these through ctypes.
+ */
+#ifndef LDGPU_H
+#define LDGPU_H
+
+#include <stdint.h>
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define LDG_OK 0
+#define LDG_EINVAL (-1)
+#define LDG_EDEVICE (-2)
+#define LDG_ENOMEM (-3)
+#define LDG_ESTATE (-4)
+
+#define LDG_SYSTEM_NTSC 0
+#define LDG_SYSTEM_PAL 1
+
+#define LDG_FMT_U8 0  /* unsigned 8-bit (cxadc)                 lddutils.py:143-144 */
+#define LDG_FMT_S16 1 /* signed 16-bit LE (.r16)                lddutils.py:146-147 */
+#define LDG_FMT_R30 2 /* 3 x 10-bit per LE uint32 (ddpack)      lddutils.py:150-173 */
+#define LDG_FMT_LDS 3 /* 4 x 10-bit per 5 bytes (DD .lds)       lddutils.py:195-229 */
+
+/* Per-read field status: why a Field is (not) valid. */
+#define LDG_FS_VALID 0    /* Field.valid == True                                  */
+#define LDG_FS_NO_VSYNC 1 /* len(vsyncs) == 0            lddecode_core.py:909-912 */
+#define LDG_FS_SHORT 2    /* 1 vsync / too few peaks      lddecode_core.py:913-924 */
+#define LDG_FS_LINELOCS 3 /* 'unable to decode frame'     lddecode_core.py:935-941 */
+#define LDG_FS_TBC 4      /* 'Unable to decode frame, skipping' :1043-1048,1178-1191 */
+#define LDG_FS_EOF 5      /* a block of the read lies beyond the capture window    */
+#define LDG_FS_CRASH 6    /* the reference raises uncaught here (documented)       */
+#define LDG_FS_PENDING 7  /* internal                                               */
+
+#define LDG_VBI_NONE (-2147483647 - 1) /* Python None in Field.vbi */
+
+#define LDG_MAX_VSYNCS 16
+
+/* Everything the host needs from one Field, lddecode_core.py:889-957,1165-1191. */
+typedef struct ldg_field_info {
+  int32_t status;       /* LDG_FS_*                                   */
+  int32_t npeaks;       /* len(Field.peaklist)                        */
+  int32_t nvsync;       /* len(Field.vsyncs)                          */
+  int32_t istop;        /* Field.istop                                */
+  int32_t linecount;    /* Field.linecount (262/263, 312/313)         */
+  int32_t nlines;       /* len(Field.linelocs) = linecount + 4        */
+  int64_t n_out;        /* demod samples in this read                 */
+  int64_t nextfieldoffset; /* Field.nextfieldoffset (relative to the read's block start) */
+  int64_t tbcstart;     /* Field.tbcstart                             */
+  double med_hsync;     /* Field.med_hsync                            */
+  double hsync_tol;     /* Field.hsync_tolerance                      */
+  int32_t vsync[LDG_MAX_VSYNCS][3]; /* Field.vsyncs rows (peak idx, line0, istop/vote) */
+  int32_t linecode[3][6];           /* Field.linecode[philips_codelines[i]] nibbles     */
+  int32_t linecode_ok[3];           /* 1 = decoded, 0 = None                            */
+  int32_t vbi_minutes, vbi_seconds, vbi_clvframe, vbi_framenr, vbi_status, vbi_isclv;
+  int32_t burst_group;  /* NTSC burst phase group of the final refine pass */
+  int32_t pad_;
+} ldg_field_info;
+
+typedef struct ldg_ctx ldg_ctx;
+
+typedef struct ldg_config {
+  int32_t system;    /* LDG_SYSTEM_NTSC / LDG_SYSTEM_PAL      */
+  int32_t device;    /* HIP device ordinal                     */
+  int32_t max_reads; /* field reads per ldg_decode_reads call  */
+  int32_t max_frames;/* frames per ldg_assemble_frames call    */
+} ldg_config;
+
+/* Scalars of the filter set / system constants (lddecode_core.py:30-117,119-279). */
+typedef struct ldg_params {
+  double freq_hz, freq, ire0, hz_ire, vsync_ire;
+  double sync_lo, sync_hi; /* iretohz(-55), iretohz(-25) */
+  double freq_arf, audio_lowfreq, audio_lfreq, audio_rfreq;
+  double line_period, fsc_mhz;
+  int32_t linelen, outlinelen, frame_lines, audio_lo0;
+  int32_t codelines[3];
+  int32_t pad_;
+} ldg_params;
+
+/* Filter tables, complex128 interleaved (re, im):
+ *   rfvideo[16384], mtf[16384], fvideo[16384], fvideo05[16384], fvideoburst[16384],
+ *   fvideopilot[16384] (PAL; may be NULL for NTSC), fpsync[16384],
+ *   audio_lfilt[1024], audio_rfilt[1024], audio_lpf2[4096];
+ * real float64: mtf_logabs[16384] = log|MTF|, mtf_arg[16384] = arg MTF. */
+typedef struct ldg_filters {
+  const double *rfvideo, *mtf, *fvideo, *fvideo05, *fvideoburst, *fvideopilot, *fpsync;
+  const double *audio_lfilt, *audio_rfilt, *audio_lpf2;
+  const double *mtf_logabs, *mtf_arg;
+} ldg_filters;
+
+int ldg_create(const ldg_config* cfg, ldg_ctx** out);
+int ldg_destroy(ldg_ctx* ctx);
+/* Human-readable description of the last error on this context. */
+const char* ldg_last_error(const ldg_ctx* ctx);
+int ldg_set_filters(ldg_ctx* ctx, const ldg_params* p, const ldg_filters* f);
+
+/* Make samples [first_sample, first_sample + nsamples) of a capture resident in
+ * HBM.  `data` points at the raw bytes of that window in the given format
+ * (first_sample must be a multiple of 3 for .r30 and of 4 for .lds).
+ * is_device != 0: `data` is already a device pointer (used in place). */
+int ldg_set_capture(ldg_ctx* ctx, const void* data, int64_t nsamples, int fmt, int64_t first_sample,
+                    int is_device);
+
+/* Demodulate and analyse n field reads: read i starts at read_starts[i] (the
+ * `start` argument of RFDecode.demod, readlen 1,000,000) with MTF level
+ * mtf[i].  Fills info[i]; pictures stay on the device, addressed by i. */
+int ldg_decode_reads(ldg_ctx* ctx, int n, const int64_t* read_starts, const double* mtf,
+                     ldg_field_info* info);
+
+/* 48 kHz audio for fields (slots of the last ldg_decode_reads) with the given
+ * starting time offsets.  pcm receives, per field, 2*count int16 samples at
+ * pcm + i * pcm_stride; counts[i], next_offsets[i] are returned. */
+int ldg_field_audio(ldg_ctx* ctx, int n, const int32_t* slots, const double* offsets, int16_t* pcm,
+                    int64_t pcm_stride, int32_t* counts, double* next_offsets);
+
+/* Interleave field pairs (top slot, bottom slot) into .tbc frames
+ * (outlinelen x frame_lines uint16).  out_is_device: `out` is a device pointer. */
+int ldg_assemble_frames(ldg_ctx* ctx, int n, const int32_t* top_slots, const int32_t* bottom_slots,
+                        uint16_t* out, int out_is_device);
+
+/* Debug / parity access to per-read device arrays of the last ldg_decode_reads.
+ * what: 0..4 demod channels (demod, demod_05, demod_sync, demod_burst, demod_pilot)
+ *       [float64, n_out]; 10,11: audio_left/right after phase 2 [float64];
+ *       20..24: linelocs1, linelocs2, linelocs3, linelocs4, final linelocs [float64];
+ *       30: burstlevel [float32]; 31: linebad [int8]; 40: dspicture [uint16]; 41: peaklist [int32].
+ * Copies up to `cap` bytes to host `dst`; returns bytes copied (>= 0) or an error. */
+int64_t ldg_debug_read(ldg_ctx* ctx, int slot, int what, void* dst, int64_t cap);
+
+/* 2D NTSC comb (comb-ntsc.cxx dim=2 defaults) on n 910x525 .tbc frames,
+ * rgb48 744x480 out.  State (aburstlev, Y-NR FIR history) persists in ctx
+ * across calls exactly as across frames of one reference comb process. */
+int ldg_comb_ntsc(ldg_ctx* ctx, int n, const uint16_t* frames, uint16_t* rgb_out, int io_is_device);
+int ldg_comb_reset(ldg_ctx* ctx);
+
+/* Library / device identification. */
+const char* ldg_version(void);
+int ldg_device_count(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* LDGPU_H */

@@ -1,0 +1,79 @@
+// Shared host/device definitions for libldgpu (not part of the public ABI).
+#pragma once
+#include <stdint.h>
+
+namespace ldg {
+
+// Overlap-save geometry of RFDecode.demod (lddecode_core.py:120-122,145,373-410).
+constexpr int BLOCKLEN = 16384;
+constexpr int BLOCKCUT = 1024;
+constexpr int BLOCKCUT_END = 32;                      // F05_offset
+constexpr int BLOCKSTEP = BLOCKLEN - BLOCKCUT - BLOCKCUT_END;   // 15328
+constexpr int HALF = BLOCKLEN / 2;                     // 8192-point complex FFTs
+constexpr int MAX_BLOCKS_PER_READ = 66;
+constexpr int READLEN = 1000000;
+constexpr int MAX_NOUT = READLEN + 1026 + 16;          // end - start + 1 (+ slack)
+constexpr int AUDIO_DIV1 = 16;                         // 40 MHz -> 2.5 MHz (blocklen / 1024)
+constexpr int AUDIO_BLOCK = 1024;
+constexpr int MAX_NAUDIO = MAX_NOUT / AUDIO_DIV1 + 16;
+constexpr int AUDIO_DIV2 = 4;                          // 2.5 MHz -> 625 kHz
+constexpr int AUDIO2_BLOCK = 4096;
+constexpr int MAX_NAUDIO2 = MAX_NAUDIO / AUDIO_DIV2 + 16;
+constexpr int MAX_PEAKS = 2048;
+constexpr int MAX_VSYNCS = 16;
+constexpr int MAX_LINES = 320;                         // linecount + 4 <= 317 (PAL)
+constexpr int MAX_OUTW = 1135;                         // PAL 4fsc line
+constexpr int LINENUM_OFF = 1024;                      // dict key offset for compute_linelocs
+constexpr int LINENUM_SPAN = 2048;
+
+// demod channel order (rec-array fields of lddecode_core.py:314-316)
+enum Chan { CH_DEMOD = 0, CH_05 = 1, CH_SYNC = 2, CH_BURST = 3, CH_PILOT = 4 };
+constexpr int MAX_CHAN = 5;
+
+// Field status codes (reason a Field is not valid; lddecode_core.py:909-941,1043-1048,1178-1191)
+enum FieldStatus {
+  FS_VALID = 0,
+  FS_NO_VSYNC = 1,        // len(vsyncs) == 0
+  FS_SHORT = 2,           // one vsync / too few peaks after the second
+  FS_LINELOCS = 3,        // exception in compute_linelocs / refine_linelocs_hsync
+  FS_TBC = 4,             // exception in burst/pilot refine or final downscale
+  FS_EOF = 5,             // a block of this read lies beyond the capture (reference: crash / None)
+  FS_CRASH = 6,           // reference would raise uncaught (e.g. vsync within first 11 peaks)
+  FS_PENDING = 7,
+};
+
+// Per-read descriptor, written by the host before a batch.
+struct ReadDesc {
+  int64_t readsample;     // 'start' argument of demod() (lddecode_core.py:373)
+  int64_t s0;             // first block sample (start - blockcut, or 0)
+  int64_t end;            // int(start + length) + 1
+  int32_t n_out;          // end - s0 + 1 (video samples)
+  int32_t n_blocks;
+  int32_t n_audio;        // ((end - s0) // 16) + 1
+  int32_t n_audio2;       // n_audio // 4
+  int32_t filt_slot;      // index of the RF filter table (RFVideo * MTF**mtf)
+  int32_t pad_;
+};
+
+// System/filter scalars (lddecode_core.py:30-117, 119-279)
+struct SysConst {
+  double freq_hz;         // 40e6
+  double freq;            // 40 (MHz; rf.freq)
+  double ire0, hz_ire, vsync_ire;
+  double sync_lo, sync_hi;        // iretohz(-55), iretohz(-25)
+  double freq_arf;                // 2.5e6
+  double audio_lowfreq;
+  double audio_lfreq, audio_rfreq;
+  double line_period;             // us
+  double fsc_mhz;
+  int32_t system;                 // 0 NTSC, 1 PAL
+  int32_t linelen;                // rf.linelen (2542 / 2560)
+  int32_t outlinelen;             // 910 / 1135
+  int32_t frame_lines;            // 525 / 625
+  int32_t n_chan;                 // 4 NTSC, 5 PAL
+  int32_t audio_lo0;              // audio_fdslice_lo.start (791)
+  int32_t codelines[3];           // philips_codelines
+  int32_t pad_;
+};
+
+}  // namespace ldg

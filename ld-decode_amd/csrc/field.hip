@@ -1,0 +1,506 @@
+// Per-field sync analysis and line location (one workgroup per field read).
+//
+// Restates Field.get_syncpeaks / get_hsync_median / is_regular_hsync /
+// determine_field / determine_vsyncs (lddecode_core.py:497-636), the
+// Field.__init__ branch that sets nextfieldoffset / istop / linecount
+// (:909-933), compute_linelocs (:638-713), refine_linelocs_hsync (:715-787),
+// decodephillipscode / processphilipscode (:814-884).
+//
+// These are data-dependent sequential scans over ~1000 sync peaks and ~263
+// lines; they run wave-parallel where the reference has array work (window
+// argmax, medians, per-line crossing searches) and on lane 0 where the
+// reference is a scalar recurrence.  Many field reads run concurrently, one
+// workgroup each.
+#include <hip/hip_runtime.h>
+#include "common.hpp"
+#include "field_rec.hpp"
+#include "pyops.hpp"
+
+using namespace ldg;
+
+namespace {
+
+struct SyncView {
+  const int32_t* pk;   // peak positions
+  const double* lv;    // ds[pk[i]]
+  int np;
+  double med, tol;
+  // is_regular_hsync (lddecode_core.py:534-542) with Python negative indexing
+  __device__ bool regular(int64_t n, int64_t len_ds, bool& err) const {
+    if (n >= np) return false;
+    int64_t idx;
+    if (!py_index(n, np, idx)) { err = true; return false; }
+    if (pk[idx] > len_ds) return false;
+    return inrange(lv[idx], med - tol, med + tol);
+  }
+  __device__ int64_t peak(int64_t n, bool& err) const {
+    int64_t idx;
+    if (!py_index(n, np, idx)) { err = true; return 0; }
+    return pk[idx];
+  }
+};
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+// Sync peaks, hsync median/tolerance, vsyncs and the Field.__init__ branch.
+// grid: n_reads workgroups of 64 threads (one wave).
+extern "C" __global__ __launch_bounds__(64) void ldg_k_sync(
+    const ReadDesc* __restrict__ reads, const double* __restrict__ video, int64_t vread_stride,
+    int64_t vchan_stride, SysConst C, FieldRec* __restrict__ recs, int32_t* __restrict__ peaks,
+    const int32_t* __restrict__ status) {
+  __shared__ int32_t s_pk[MAX_PEAKS];
+  __shared__ double s_lv[MAX_PEAKS];
+  __shared__ double s_tmp[2 * MAX_PEAKS];
+  const int lane = threadIdx.x;
+  const int slot = blockIdx.x;
+  FieldRec* R = recs + slot;
+  const ReadDesc rd = reads[slot];
+  if (lane == 0) R->n_out = rd.n_out;
+  if (status[slot] == FS_EOF) {
+    if (lane == 0) { R->status = FS_EOF; R->npeaks = 0; R->nvsync = 0; }
+    return;
+  }
+  const double* ds = video + (int64_t)slot * vread_stride + (int64_t)CH_SYNC * vchan_stride;
+  const int64_t len = rd.n_out;
+  const int linelen = C.linelen;
+  const int win = linelen / 2;                     // inlinelen // 2
+  const int jump = (int)((double)linelen * .4);    // int(rf.linelen * .4)
+  const int64_t stop = len - 2 * (int64_t)linelen;
+
+  // ---- get_syncpeaks: sequential window-argmax walk --------------------------
+  int np = 0;
+  bool overflow = false;
+  int64_t i = 0;
+  while (i < stop) {
+    const int64_t wend = (i + win < len) ? i + win : len;
+    double best = -__builtin_inf();
+    int64_t bidx = 0x7fffffffffffffffLL;
+    for (int64_t k = i + lane; k < wend; k += 64) {
+      const double v = ds[k];
+      if (v > best) { best = v; bidx = k; }
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+      const double ov = __shfl_xor(best, o);
+      const int64_t oi = __shfl_xor(bidx, o);
+      if (ov > best || (ov == best && oi < bidx)) { best = ov; bidx = oi; }
+    }
+    if (best > .2) {
+      if (np < MAX_PEAKS) {
+        if (lane == 0) { s_pk[np] = (int32_t)bidx; s_lv[np] = best; }
+        np++;
+      } else {
+        overflow = true;
+        break;
+      }
+      i = bidx + jump;
+    } else {
+      i += win;
+    }
+  }
+  __syncthreads();
+  if (lane == 0) R->npeaks = np;
+  for (int k = lane; k < np; k += 64) peaks[(int64_t)slot * MAX_PEAKS + k] = s_pk[k];
+  if (overflow) {
+    if (lane == 0) { R->status = FS_CRASH; R->nvsync = 0; }
+    return;
+  }
+  if (lane != 0) return;
+
+  // ---- determine_vsyncs (lane 0) ---------------------------------------------
+  R->nvsync = 0;
+  R->status = FS_PENDING;
+  int64_t vs[MAX_VSYNCS][3];
+  int nf = 0;
+  double med = 0, tol = 0;
+  bool err = false;
+  if (np >= 200) {
+    int nh = 0;
+    for (int k = 0; k < np; k++)
+      if (inrange(s_lv[k], 0.6, 0.8)) s_tmp[nh++] = s_lv[k];
+    // np.std over the list in peak order, then np.median (sorts a copy)
+    double sd;
+    if (nh > 0) {
+      double* sq = s_tmp + nh;                       // scratch after the levels
+      sd = np_std(s_tmp, nh, sq);
+      isort(s_tmp, nh);
+      med = sorted_median(s_tmp, nh);
+    } else {
+      sd = __builtin_nan("");
+      med = __builtin_nan("");
+    }
+    const double t2 = sd * 2;
+    tol = (.01 > t2) ? .01 : t2;                     // Python max(t2, .01): keeps t2 unless .01 > t2
+    R->med_hsync = med;
+    R->hsync_tol = tol;
+    SyncView V{s_pk, s_lv, np, med, tol};
+    double prev = 1.0;
+    for (int k = 0; k < np; k++) {
+      const double lvl = s_lv[k];
+      if (lvl > .9 && prev < med - (tol * 2)) {
+        if (k < 11) { R->status = FS_CRASH; return; }     // determine_field -> None, unpacked
+        // determine_field (lddecode_core.py:544-588)
+        int vote = 0;
+        int64_t line0 = 0;
+        bool have0 = false;
+        int64_t gap1 = 0;
+        for (int64_t q = k - 1; q > k - 20; q--) {
+          if (V.regular(q, len, err)) {
+            line0 = q; have0 = true;
+            gap1 = V.peak(line0 + 1, err) - V.peak(line0, err);
+            break;
+          }
+        }
+        if (have0 && (double)gap1 > linelen * .75) vote -= 1;
+        for (int64_t q = k; q < k + 20; q++) {
+          if (V.regular(q, len, err)) {
+            const int64_t gap2 = V.peak(q, err) - V.peak(q - 1, err);
+            if ((double)gap2 > linelen * .75) vote += (C.system == 0) ? 1 : -1;
+            break;
+          }
+        }
+        if (C.system == 1) vote += 1;
+        if (err) { R->status = FS_CRASH; return; }
+        if (have0) {
+          if (nf >= MAX_VSYNCS) { R->status = FS_CRASH; return; }
+          vs[nf][0] = k; vs[nf][1] = line0; vs[nf][2] = vote;
+          nf++;
+        }
+      }
+      prev = lvl;
+    }
+    if (nf >= 2) {
+      // vote repair + line0 override + bool conversion, in place like the numpy array va
+      int64_t orig[MAX_VSYNCS];
+      for (int q = 0; q < nf; q++) orig[q] = vs[q][2];
+      for (int q = 0; q < nf; q++) {
+        if (vs[q][2] == 0) {
+          vs[q][1] = -1;
+          if ((q < nf - 1) && orig[q + 1] != 0) vs[q][2] = -vs[q + 1][2];
+          else if ((q >= 1) && orig[q - 1] != 0) vs[q][2] = -vs[q - 1][2];
+        }
+        if (vs[q][1] <= 0) vs[q][1] = vs[q][0] - ((C.system == 1) ? 6 : 7);
+        vs[q][2] = vs[q][2] < 0 ? 1 : 0;
+      }
+    }
+  }
+  R->nvsync = nf;
+  for (int q = 0; q < nf && q < MAX_VSYNCS; q++) {
+    R->vsync[q][0] = (int32_t)vs[q][0]; R->vsync[q][1] = (int32_t)vs[q][1]; R->vsync[q][2] = (int32_t)vs[q][2];
+  }
+  SyncView V{s_pk, s_lv, np, med, tol};
+  // ---- Field.__init__ branch (lddecode_core.py:909-933) ------------------------
+  if (nf == 0) {
+    R->nextfieldoffset = (int64_t)C.linelen * 200;
+    R->status = FS_NO_VSYNC;
+    return;
+  }
+  if (nf == 1 || np < vs[1][1] + 4) {
+    const int64_t jumpto = V.peak(vs[0][1] - 10, err);
+    if (err) { R->status = FS_CRASH; return; }
+    R->nextfieldoffset = jumpto;
+    if (jumpto == 0) R->nextfieldoffset = (int64_t)C.linelen * 240;
+    R->status = FS_SHORT;
+    return;
+  }
+  const int64_t nfo = V.peak(vs[1][1] - 10, err);
+  if (err) { R->status = FS_CRASH; return; }
+  R->nextfieldoffset = nfo;
+  R->tbcstart = nfo;
+  R->istop = (int32_t)vs[0][2];
+  R->linecount = C.frame_lines / 2 + (vs[0][2] ? 1 : 0);
+  R->nlines = R->linecount + 4;
+  R->status = FS_PENDING;
+}
+
+// ---------------------------------------------------------------------------
+// compute_linelocs (lddecode_core.py:638-713).  grid: n_reads x 64 threads; lane 0.
+extern "C" __global__ __launch_bounds__(64) void ldg_k_linelocs(
+    const double* __restrict__ video, int64_t vread_stride, int64_t vchan_stride, SysConst C,
+    FieldRec* __restrict__ recs, const int32_t* __restrict__ peaks, double* __restrict__ lines,
+    int8_t* __restrict__ bad) {
+  __shared__ double s_key[LINENUM_SPAN];
+  __shared__ uint8_t s_has[LINENUM_SPAN];
+  __shared__ uint8_t s_orig[LINENUM_SPAN];
+  __shared__ double s_lv[MAX_PEAKS];
+  const int lane = threadIdx.x;
+  const int slot = blockIdx.x;
+  FieldRec* R = recs + slot;
+  if (R->status != FS_PENDING) return;
+  const int np = R->npeaks;
+  const int32_t* pk = peaks + (int64_t)slot * MAX_PEAKS;
+  const double* ds = video + (int64_t)slot * vread_stride + (int64_t)CH_SYNC * vchan_stride;
+  for (int k = lane; k < LINENUM_SPAN; k += 64) { s_has[k] = 0; s_orig[k] = 0; }
+  for (int k = lane; k < np; k += 64) s_lv[k] = ds[pk[k]];
+  __syncthreads();
+  if (lane != 0) return;
+
+  const double inl = (double)C.linelen;
+  SyncView V{pk, s_lv, np, R->med_hsync, R->hsync_tol};
+  const int64_t v01 = R->vsync[0][1], v11 = R->vsync[1][1];
+  const int linecount = R->linecount;
+  bool err = false;
+  // sliding window of the last 25 accepted line lengths, kept sorted
+  double win[25];
+  double ring[25];
+  int nlens = 1, rpos = 0;
+  win[0] = inl; ring[0] = inl;
+  int64_t prev_idx = -1, prev_num = 0;
+  for (int64_t i = 0; i < v11; i++) {
+    const int wn = nlens < 25 ? nlens : 25;
+    const double med_len = sorted_median(win, wn);
+    if (V.regular(i, 0x7fffffffffffLL, err)) {
+      int64_t num;
+      if (prev_idx >= 0) {
+        const int64_t gap = (int64_t)pk[i] - pk[prev_idx];
+        if (inrange((double)gap / inl, .98, 1.02)) {
+          // lens.append(gap): update the sorted window of the last 25
+          const double g = (double)gap;
+          if (nlens >= 25) {
+            const double old = ring[rpos];
+            int p = 0;
+            while (p < 25 && win[p] != old) p++;
+            for (int q = p; q < 24; q++) win[q] = win[q + 1];
+            ring[rpos] = g; rpos = (rpos + 1) % 25;
+            int q = 23;
+            while (q >= 0 && win[q] > g) { win[q + 1] = win[q]; q--; }
+            win[q + 1] = g;
+          } else {
+            ring[nlens] = g;
+            int q = nlens - 1;
+            while (q >= 0 && win[q] > g) { win[q + 1] = win[q]; q--; }
+            win[q + 1] = g;
+            if (nlens + 1 == 25) rpos = 0;
+          }
+          nlens++;
+          num = prev_num + 1;
+        } else {
+          num = prev_num + (int64_t)np_round((double)(pk[i] - pk[prev_idx]) / med_len);
+        }
+      } else {
+        const int64_t base_peak = V.peak(v01, err);   // plist[vsyncs[0][1]], evaluated lazily
+        num = (int64_t)np_round((double)(pk[i] - base_peak) / med_len);
+      }
+      const int64_t key = num + LINENUM_OFF;
+      if (key < 0 || key >= LINENUM_SPAN) { R->status = FS_LINELOCS; return; }
+      s_key[key] = (double)pk[i];
+      s_has[key] = 1; s_orig[key] = 1;
+      prev_idx = i; prev_num = num;
+    }
+  }
+  if (err) { R->status = FS_CRASH; return; }
+  // fill missing line numbers 1..linecount+4
+  double* L1 = lines + (int64_t)slot * LINES_STRIDE + LL1 * MAX_LINES;
+  int8_t* B1 = bad + (int64_t)slot * MAX_LINES;
+  for (int l = 1; l < linecount + 5; l++) {
+    const int kl = l + LINENUM_OFF;
+    if (s_orig[kl]) continue;
+    int pv = -100000, nv = -100000;
+    for (int q = l; q > -10; q--) if (s_orig[q + LINENUM_OFF]) { pv = q; break; }
+    for (int q = l; q < linecount + 1; q++) if (s_orig[q + LINENUM_OFF]) { nv = q; break; }
+    double v;
+    if (pv == -100000) {
+      if (nv == -100000) { R->status = FS_LINELOCS; return; }   // linelocs[None] KeyError
+      v = s_key[nv + LINENUM_OFF] - (inl * (double)(nv - l));
+    } else if (nv != -100000) {
+      const double step = (s_key[nv + LINENUM_OFF] - s_key[pv + LINENUM_OFF]) / (double)(nv - pv);
+      v = s_key[pv + LINENUM_OFF] + (step * (double)(l - pv));
+    } else {
+      const int kprev = pv - 1 + LINENUM_OFF;
+      if (!s_has[kprev]) { R->status = FS_LINELOCS; return; }   // linelocs2[prev_valid - 1] KeyError
+      const double step = s_key[pv + LINENUM_OFF] - s_key[kprev];
+      v = s_key[pv + LINENUM_OFF] + (step * (double)(l - pv));
+    }
+    s_key[kl] = v;
+    s_has[kl] = 1;
+  }
+  for (int l = 1; l < linecount + 5; l++) {
+    L1[l - 1] = s_key[l + LINENUM_OFF];
+    B1[l - 1] = (l - 1 < 10) ? 0 : (s_orig[l + LINENUM_OFF] ? 0 : 1);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// refine_linelocs_hsync (lddecode_core.py:715-787).
+// grid: n_reads x 256 threads: per-line crossing searches in parallel, then
+// the sequential bad-line extrapolation and the two end fix-ups on thread 0.
+extern "C" __global__ __launch_bounds__(256) void ldg_k_hsync(
+    const double* __restrict__ video, int64_t vread_stride, int64_t vchan_stride, SysConst C,
+    FieldRec* __restrict__ recs, double* __restrict__ lines, int8_t* __restrict__ bad) {
+  __shared__ double s_v[MAX_LINES];
+  __shared__ int8_t s_bad[MAX_LINES];
+  __shared__ int s_err;
+  const int tid = threadIdx.x;
+  const int slot = blockIdx.x;
+  FieldRec* R = recs + slot;
+  if (R->status != FS_PENDING) return;
+  const int nl = R->nlines;
+  const double* d05 = video + (int64_t)slot * vread_stride + (int64_t)CH_05 * vchan_stride;
+  const int64_t len = R->n_out;
+  const double* L1 = lines + (int64_t)slot * LINES_STRIDE + LL1 * MAX_LINES;
+  double* L2 = lines + (int64_t)slot * LINES_STRIDE + LL2 * MAX_LINES;
+  int8_t* B = bad + (int64_t)slot * MAX_LINES;
+  const double fr = C.freq;
+  auto hz = [&](double ire) { return C.ire0 + (C.hz_ire * ire); };
+  if (tid == 0) s_err = 0;
+  __syncthreads();
+  for (int i = tid; i < nl; i += 256) {
+    double v = L1[i];
+    bool lb = B[i] != 0;
+    if (i < 9) v -= 200;
+    const double ll1 = v;
+    double zc;
+    const int rc = calczc(d05, len, v, hz(-20), 400, &zc);
+    if (rc < 0) { atomicOr(&s_err, 1); continue; }
+    if (rc == 0 && !lb) {
+      v = zc;
+      if (i >= 10) {
+        int64_t a1, b1, ah, bh, ab, bb;
+        py_slice(py_int(ll1 - (fr * 2)), py_int(ll1 + (fr * 2)), len, a1, b1);
+        py_slice(py_int(zc - (fr * 1)), py_int(zc + (fr * 3)), len, ah, bh);
+        py_slice(py_int(zc + (fr * 1)), py_int(zc + (fr * 3)), len, ab, bb);
+        auto mn = [&](int64_t a, int64_t b) { double m = d05[a]; for (int64_t k = a + 1; k < b; k++) m = fmin(m, d05[k]); return m; };
+        auto mx = [&](int64_t a, int64_t b) { double m = d05[a]; for (int64_t k = a + 1; k < b; k++) m = fmax(m, d05[k]); return m; };
+        // evaluation order of the reference's `or` chain; an empty window raises
+        bool isbad = false, raised = false;
+        auto grp = [&](int64_t a, int64_t b, double lo, double hi) -> bool {
+          if (a >= b) { raised = true; return true; }
+          if (mn(a, b) < lo) return true;
+          return mx(a, b) > hi;
+        };
+        if (grp(ah, bh, hz(-60), hz(20))) isbad = true;
+        else if (grp(a1, b1, hz(-60), hz(100))) isbad = true;
+        else if (grp(ab, bb, hz(-10), hz(10))) isbad = true;
+        if (raised) { atomicOr(&s_err, 1); continue; }
+        if (isbad) {
+          lb = true;
+        } else {
+          const int64_t wl = bh - ah;
+          double tmp[20];
+          int64_t lo, hi;
+          py_slice(0, 20, wl, lo, hi);
+          for (int64_t k = lo; k < hi; k++) tmp[k - lo] = d05[ah + k];
+          const double low = np_mean(tmp, (int)(hi - lo));
+          py_slice(100, 120, wl, lo, hi);
+          for (int64_t k = lo; k < hi; k++) tmp[k - lo] = d05[ah + k];
+          const double high = np_mean(tmp, (int)(hi - lo));
+          double zc2;
+          const int rc2 = calczc(d05 + ah, wl, 0, (low + high) / 2, wl, &zc2);
+          if (rc2 != 0) { atomicOr(&s_err, 1); continue; }   // None += ... -> TypeError
+          zc2 += ((double)py_int(zc) - (fr * 1));
+          if (fabs(zc2 - zc) < (fr / 4)) v = zc2;
+          else lb = true;
+        }
+      }
+    } else {
+      lb = true;
+    }
+    s_v[i] = v;
+    s_bad[i] = lb ? 1 : 0;
+  }
+  __syncthreads();
+  if (tid != 0) return;
+  if (s_err) { R->status = FS_LINELOCS; return; }
+  for (int i = 0; i < nl; i++) {
+    if (i < 10) s_v[i] += 4.72 * fr;
+    if (i > 10 && s_bad[i]) {
+      const double gap = s_v[i - 1] - s_v[i - 2];
+      s_v[i] = s_v[i - 1] + gap;
+    }
+  }
+  const double lo = C.linelen - (fr * .2), hi = C.linelen + (fr * .2);
+  for (int i = 9; i >= 0; i--) {
+    double gap = s_v[i + 1] - s_v[i];
+    if (!inrange(gap, lo, hi)) gap = C.linelen;
+    s_v[i] = s_v[i + 1] - gap;
+  }
+  for (int i = nl - 10; i < nl; i++) {
+    double gap = s_v[i] - s_v[i - 1];
+    if (!inrange(gap, lo, hi)) gap = C.linelen;
+    s_v[i] = s_v[i - 1] + gap;
+  }
+  for (int i = 0; i < nl; i++) { L2[i] = s_v[i]; B[i] = s_bad[i]; }
+}
+
+// ---------------------------------------------------------------------------
+// Philips VBI decode (lddecode_core.py:814-884).  grid: n_reads x 64; lanes 0..2
+// decode one code line each, lane 0 then interprets them.
+extern "C" __global__ __launch_bounds__(64) void ldg_k_philips(
+    const double* __restrict__ video, int64_t vread_stride, int64_t vchan_stride, SysConst C,
+    FieldRec* __restrict__ recs, const double* __restrict__ lines) {
+  __shared__ int32_t s_code[3][6];
+  __shared__ int32_t s_ok[3];
+  const int lane = threadIdx.x;
+  const int slot = blockIdx.x;
+  FieldRec* R = recs + slot;
+  if (R->status != FS_PENDING) return;
+  const double* dm = video + (int64_t)slot * vread_stride + (int64_t)CH_DEMOD * vchan_stride;
+  const int64_t len = R->n_out;
+  const double* L2 = lines + (int64_t)slot * LINES_STRIDE + LL2 * MAX_LINES;
+  const double fr = C.freq;
+  const double thr = C.ire0 + (C.hz_ire * 50);
+  if (lane < 3) {
+    int ok = 0;
+    const int ln = C.codelines[lane];
+    const double start = L2[ln];
+    double cur;
+    int rc = calczc(dm, len, (double)py_int(start + 2 * fr), thr, py_int(12 * fr), &cur);
+    int n = 0;
+    int bits[24];
+    double first = 0, prevz = 0, gmin = __builtin_inf(), gmax = -__builtin_inf();
+    bool crash = false;
+    while (rc == 0) {
+      int64_t bi;
+      if (!py_index(py_int(cur - 0.5 * fr), len, bi)) { crash = true; break; }
+      if (n < 24) bits[n] = dm[bi] < thr ? 1 : 0;
+      if (n > 0) {
+        const double g = (cur - prevz) / fr;
+        gmin = fmin(gmin, g); gmax = fmax(gmax, g);
+      } else {
+        first = cur;
+      }
+      prevz = cur;
+      n++;
+      if (n > 100000) break;
+      rc = calczc(dm, len, cur + 1.9 * fr, thr, py_int(0.2 * fr), &cur);
+    }
+    (void)first;
+    if (rc < 0 || crash) ok = -1;
+    else if (n == 24 && gmin > 1.85 && gmax < 2.15) {
+      ok = 1;
+      for (int b = 0; b < 6; b++)
+        s_code[lane][b] = (bits[4 * b] << 3) | (bits[4 * b + 1] << 2) | (bits[4 * b + 2] << 1) | bits[4 * b + 3];
+    }
+    s_ok[lane] = ok;
+  }
+  __syncthreads();
+  if (lane != 0) return;
+  for (int q = 0; q < 3; q++)
+    if (s_ok[q] < 0) { R->status = FS_CRASH; return; }   // IndexError outside the reference's try
+  int minutes = VBI_NONE, seconds = VBI_NONE, clvframe = VBI_NONE, framenr = VBI_NONE, statusv = VBI_NONE;
+  int isclv = 0;
+  for (int q = 0; q < 3; q++) {
+    R->linecode_ok[q] = s_ok[q];
+    for (int b = 0; b < 6; b++) R->linecode[q][b] = s_ok[q] ? s_code[q][b] : 0;
+    if (!s_ok[q]) continue;
+    const int32_t* lc = s_code[q];
+    if (lc[0] == 15 && lc[2] == 13) {
+      minutes = 60 * lc[1] + lc[4] * 10 + lc[5];
+      isclv = 1;
+    } else if (lc[0] == 15) {
+      framenr = (lc[1] & 7) * 10000 + (lc[2] * 1000) + (lc[3] * 100) + (lc[4] * 10) + lc[5];
+    } else {
+      const int h = (lc[0] << 20) | (lc[1] << 16) | (lc[2] << 12) | (lc[3] << 8) | (lc[4] << 4) | lc[5];
+      if (lc[2] == 0xE) {
+        seconds = (lc[1] - 10) * 10 + lc[3];
+        clvframe = lc[4] * 10 + lc[5];
+        isclv = 1;
+      }
+      const int htop = h >> 12;
+      if (htop == 0x8dc || htop == 0x8ba) statusv = h;
+      if (h == 0x87ffff) isclv = 1;
+    }
+  }
+  R->vbi_minutes = minutes; R->vbi_seconds = seconds; R->vbi_clvframe = clvframe;
+  R->vbi_framenr = framenr; R->vbi_status = statusv; R->vbi_isclv = isclv;
+}

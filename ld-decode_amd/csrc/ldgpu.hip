@@ -1,0 +1,6 @@
+// libldgpu unity build: all device code + the C ABI in one translation unit.
+#include "demod.hip"
+#include "field.hip"
+#include "tbc.hip"
+#include "comb.hip"
+#include "abi.inc"

@@ -1,0 +1,140 @@
+// Device restatements of the numpy / Python primitives the reference's
+// per-field logic is built from, with their exact semantics (summation order,
+// first-occurrence argmax, Python slicing / negative indexing, banker's
+// rounding).  Used by field.hip and tbc.hip.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace ldg {
+
+// numpy pairwise summation (numpy/_core/src/umath/loops_utils.h.src,
+// PW_BLOCKSIZE = 128, 8-way unrolled); np.sum/np.mean of a float64 array.
+__device__ inline double pw_block(const double* a, int n) {
+  if (n < 8) {
+    double r = -0.0;
+    for (int i = 0; i < n; i++) r += a[i];
+    return r;
+  }
+  double r[8];
+  for (int j = 0; j < 8; j++) r[j] = a[j];
+  int i = 8;
+  for (; i < n - (n % 8); i += 8)
+    for (int j = 0; j < 8; j++) r[j] += a[i + j];
+  double res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+  for (; i < n; i++) res += a[i];
+  return res;
+}
+
+template <int L> __device__ inline double pw_sum_l(const double* a, int n) {
+  if (n <= 128) return pw_block(a, n);
+  int n2 = n / 2;
+  n2 -= n2 % 8;
+  return pw_sum_l<L - 1>(a, n2) + pw_sum_l<L - 1>(a + n2, n - n2);
+}
+template <> __device__ inline double pw_sum_l<0>(const double* a, int n) { return pw_block(a, n); }
+
+__device__ inline double pw_sum(const double* a, int n) { return 0.0 + pw_sum_l<8>(a, n); }
+__device__ inline double np_mean(const double* a, int n) { return pw_sum(a, n) / (double)n; }
+
+// np.std (ddof 0): mean, deviations, squares, pairwise sum, / n, sqrt.  `tmp` >= n doubles.
+__device__ inline double np_std(const double* a, int n, double* tmp) {
+  const double m = pw_sum(a, n) / (double)n;
+  for (int i = 0; i < n; i++) { const double d = a[i] - m; tmp[i] = d * d; }
+  return sqrt(pw_sum(tmp, n) / (double)n);
+}
+
+__device__ inline bool inrange(double a, double lo, double hi) { return (a >= lo) && (a <= hi); }
+
+// np.round / Python round on doubles: half to even.
+__device__ inline double np_round(double x) { return rint(x); }
+
+// Python slice [a:b] of a length-n sequence -> [lo, hi) (empty if lo >= hi).
+__device__ inline void py_slice(int64_t a, int64_t b, int64_t n, int64_t& lo, int64_t& hi) {
+  if (a < 0) { a += n; if (a < 0) a = 0; } else if (a > n) a = n;
+  if (b < 0) { b += n; if (b < 0) b = 0; } else if (b > n) b = n;
+  lo = a; hi = b;
+}
+
+// Python index (negative wraps); returns false on IndexError.
+__device__ inline bool py_index(int64_t i, int64_t n, int64_t& out) {
+  if (i < 0) i += n;
+  if (i < 0 || i >= n) return false;
+  out = i;
+  return true;
+}
+
+// int() of a Python float: truncation toward zero.
+__device__ inline int64_t py_int(double x) { return (int64_t)x; }
+
+// lddutils.calczc (lddutils.py:265-303) with edge='both', reverse=False.
+// Returns 0 and sets *res on success, 1 for "None", -1 for an IndexError.
+__device__ inline int calczc(const double* data, int64_t len, double start_offset, double target, int64_t count,
+                             double* res) {
+  const int64_t s = py_int(start_offset);
+  const int64_t n = count + 1;
+  int64_t si;
+  if (!py_index(s, len, si)) return -1;         // data[start_offset] IndexError
+  const bool rising = data[si] < target;
+  int64_t lo, hi;
+  py_slice(s, s + n, len, lo, hi);
+  int64_t hit = -1;
+  for (int64_t k = lo; k < hi; k++) {
+    const double v = data[k];
+    if (rising ? (v >= target) : (v <= target)) { hit = k - lo; break; }
+  }
+  if (hit < 0) return 1;
+  const int64_t x = s + hit;
+  if (x == 0) return 1;
+  int64_t ia, ib;
+  if (!py_index(x - 1, len, ia) || !py_index(x, len, ib)) return -1;
+  const double a = data[ia] - target;
+  const double b = data[ib] - target;
+  *res = (double)(x - 1) + ((-a) / ((-a) + b));
+  return 0;
+}
+
+// Sorted-window median helper: median of a[0..n) already sorted ascending.
+__device__ inline double sorted_median(const double* a, int n) {
+  if (n <= 0) return __builtin_nan("");
+  if (n & 1) return a[n / 2];
+  return (a[n / 2 - 1] + a[n / 2]) / 2.0;
+}
+
+// In-place insertion sort (small n, one thread).  NaNs sort last like np.sort.
+__device__ inline void isort(double* a, int n) {
+  for (int i = 1; i < n; i++) {
+    const double v = a[i];
+    int j = i - 1;
+    while (j >= 0 && (a[j] > v || (a[j] != a[j] && v == v))) { a[j + 1] = a[j]; j--; }
+    a[j + 1] = v;
+  }
+}
+
+// np.median of a[0..n) with a scratch copy (one thread).
+__device__ inline double np_median(const double* a, int n, double* tmp) {
+  if (n <= 0) return __builtin_nan("");
+  for (int i = 0; i < n; i++) tmp[i] = a[i];
+  isort(tmp, n);
+  for (int i = 0; i < n; i++) if (tmp[i] != tmp[i]) return __builtin_nan("");
+  return sorted_median(tmp, n);
+}
+
+// Block-wide bitonic sort of a[0..npow2) in LDS (npow2 a power of two, pad with +inf).
+__device__ inline void block_bitonic_sort(double* a, int npow2, int tid, int nthreads) {
+  for (int k = 2; k <= npow2; k <<= 1) {
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      for (int i = tid; i < npow2; i += nthreads) {
+        const int ixj = i ^ j;
+        if (ixj > i) {
+          const double x = a[i], y = a[ixj];
+          const bool up = (i & k) == 0;
+          if (up ? (x > y) : (x < y)) { a[i] = y; a[ixj] = x; }
+        }
+      }
+      __syncthreads();
+    }
+  }
+}
+
+}  // namespace ldg

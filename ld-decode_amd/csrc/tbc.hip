@@ -1,0 +1,493 @@
+// Time-base correction: per-line spline resampling to 4fsc, NTSC colour-burst
+// line refinement, final IRE -> uint16 .tbc lines, 48 kHz audio, frame assembly.
+//
+// Restates Field.downscale + lddutils.scale (lddecode_core.py:789-812,
+// lddutils.py:83-97), FieldNTSC.refine_linelocs_burst / apply_offsets /
+// downscale(final) (lddecode_core.py:1054-1162), FieldPAL.downscale(final)
+// (:1023-1035), downscale_audio (:431-484) and Framer.formatoutput (:1238-1252).
+//
+// Spline: scipy splrep(s=0) on unit-spaced points is the not-a-knot cubic
+// interpolant; it is solved exactly (no truncation) in second-derivative form
+// with a Thomas sweep, ONE LANE PER LINE: 64 lines per wave run their
+// recurrences side by side, and the Thomas scratch is lane-interleaved
+// (dp[t*64 + lane]) so every step is a coalesced 512-byte access.
+#include <hip/hip_runtime.h>
+#include "common.hpp"
+#include "field_rec.hpp"
+#include "pyops.hpp"
+
+using namespace ldg;
+
+namespace {
+
+constexpr int SPL_MAXN = 2816;                 // max points per line (NTSC ~2545, PAL ~2563)
+constexpr int LINE_GROUPS = (MAX_LINES + 63) / 64;
+
+struct CTab { double v[17]; };
+constexpr CTab make_ctab() {
+  CTab t{};
+  double c = 0.25;
+  for (int i = 0; i < 17; i++) { t.v[i] = c; c = 1.0 / (4.0 - c); }
+  return t;
+}
+__constant__ CTab g_ctab = make_ctab();        // Thomas c'_t for diag 4 / off-diag 1 (fixed point from t=14)
+__device__ __forceinline__ double ctab(int64_t t) { return g_ctab.v[t < 16 ? t : 16]; }
+
+// Not-a-knot cubic spline through y[j] = buf[ib + j], j = 0..n, evaluated at
+// x_o = o*step + x0 (numpy linspace(begin-ib, end-ib, W+1) arithmetic) for o in
+// [o_lo, o_hi), visiting o in descending order: sink(o, value).
+// dp: this lane's scratch, element t at dp[t * 64].  Returns 0, or -1 where
+// splrep would raise (too few / missing points).
+template <class Sink>
+__device__ int spline_eval(const double* __restrict__ buf, int64_t len, double begin, double end, int W, int o_lo,
+                           int o_hi, double* __restrict__ dp, Sink&& sink) {
+  const int64_t ib = py_int(begin), ie = py_int(end);
+  const int64_t n = ie - ib;
+  if (ib < 0 || n < 6 || n >= SPL_MAXN || ib + n + 1 > len) return -1;
+  const double* y = buf + ib;
+  auto rr = [&](int64_t j) { return 6.0 * ((y[j + 1] - y[j]) - (y[j] - y[j - 1])); };
+  const double M1 = rr(1) / 6.0, Mn1 = rr(n - 1) / 6.0;   // not-a-knot rows folded in
+  const int64_t N = n - 3;                                 // unknowns M_2 .. M_{n-2}
+  double dprev = 0.0;
+  for (int64_t t = 0; t < N; t++) {
+    double rhs = rr(t + 2);
+    if (t == 0) rhs -= M1;
+    if (t == N - 1) rhs -= Mn1;
+    const double d = (rhs - dprev) * ctab(t);
+    dp[t * 64] = d;
+    dprev = d;
+  }
+  const double x0 = begin - (double)ib;
+  const double span = end - begin;
+  const double step = ((span + x0) - x0) / (double)W;
+  const double Mn2 = dp[(N - 1) * 64];
+  double Mk1 = 2.0 * Mn1 - Mn2;   // M_n
+  double M2 = 0.0;
+  int o = o_hi - 1;
+  for (int64_t k = n - 1; k >= 0 && o >= o_lo; k--) {
+    double Mk;
+    if (k == n - 1) Mk = Mn1;
+    else if (k >= 2) {
+      const int64_t t = k - 2;
+      Mk = (t == N - 1) ? dp[t * 64] : dp[t * 64] - ctab(t) * Mk1;
+    } else if (k == 1) Mk = M1;
+    else Mk = 2.0 * M1 - M2;
+    if (k == 2) M2 = Mk;
+    const double yk = y[k], yk1 = y[k + 1];
+    while (o >= o_lo) {
+      double x = (double)o * step;
+      x = x + x0;
+      if (k > 0 && x < (double)k) break;
+      const double a = (double)(k + 1) - x, b = x - (double)k;
+      const double v = Mk * a * a * a / 6.0 + Mk1 * b * b * b / 6.0 + (yk - Mk / 6.0) * a + (yk1 - Mk1 / 6.0) * b;
+      sink(o, v);
+      o--;
+    }
+    Mk1 = Mk;
+  }
+  return 0;
+}
+
+// strided numpy pairwise sum (same order as pw_sum over a[0], a[st], ...)
+__device__ inline double pwb_s(const double* a, int n, int st) {
+  if (n < 8) {
+    double r = -0.0;
+    for (int i = 0; i < n; i++) r += a[i * st];
+    return r;
+  }
+  double r[8];
+  for (int j = 0; j < 8; j++) r[j] = a[j * st];
+  int i = 8;
+  for (; i < n - (n % 8); i += 8)
+    for (int j = 0; j < 8; j++) r[j] += a[(i + j) * st];
+  double res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+  for (; i < n; i++) res += a[i * st];
+  return 0.0 + res;
+}
+
+__device__ inline int calczc_s(const double* d, int len, int s, double target, int count, int st, double* res) {
+  const bool rising = d[s * st] < target;
+  const int hi = (s + count + 1 < len) ? s + count + 1 : len;
+  int hit = -1;
+  for (int k = s; k < hi; k++) {
+    const double v = d[k * st];
+    if (rising ? (v >= target) : (v <= target)) { hit = k - s; break; }
+  }
+  if (hit < 0) return 1;
+  const int x = s + hit;
+  if (x == 0) return 1;
+  const double a = d[(x - 1) * st] - target, b = d[x * st] - target;
+  *res = (double)(x - 1) + ((-a) / ((-a) + b));
+  return 0;
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+// Burst pass, per (read, line): resample demod_burst over [li[l], li[l+1]] to
+// 4fsc pixels 20..59 (lineoffset 0, wow-scaled), then the per-line part of
+// refine_linelocs_burst (lddecode_core.py:1069-1110).
+// grid: n_reads * LINE_GROUPS workgroups of 64 threads; lane = line.
+extern "C" __global__ __launch_bounds__(64) void ldg_k_burst_lines(
+    const double* __restrict__ video, int64_t vread_stride, int64_t vchan_stride, SysConst C,
+    FieldRec* __restrict__ recs, double* __restrict__ lines, float* __restrict__ blevel,
+    double* __restrict__ scratch, int pass) {
+  __shared__ double s_ba[40 * 64];
+  __shared__ double s_t[40 * 64];
+  const int lane = threadIdx.x;
+  const int slot = blockIdx.x / LINE_GROUPS;
+  const int grp = blockIdx.x % LINE_GROUPS;
+  FieldRec* R = recs + slot;
+  if (R->status != FS_PENDING) return;
+  const int l = grp * 64 + lane;
+  const int nl = R->nlines, lc = R->linecount;
+  double* LN = lines + (int64_t)slot * LINES_STRIDE;
+  const double* li = LN + (pass == 0 ? LL2 : LL3) * MAX_LINES;
+  double* pv0 = LN + PAVG0 * MAX_LINES;
+  double* pv1 = LN + PAVG1 * MAX_LINES;
+  float* lvl = blevel + (int64_t)slot * MAX_LINES;
+  if (l >= nl) return;
+  if (l >= lc) { pv0[l] = 0.0; pv1[l] = 0.0; lvl[l] = 0.0f; return; }
+  const double* bur = video + (int64_t)slot * vread_stride + (int64_t)CH_BURST * vchan_stride;
+  double* dp = scratch + (((int64_t)slot * LINE_GROUPS + grp) * SPL_MAXN) * 64 + lane;
+  double* ba = s_ba + lane;
+  double* tt = s_t + lane;
+  const double b0 = li[l], b1 = li[l + 1];
+  const double wow = (b1 - b0) / (double)C.linelen;
+  const int W = C.outlinelen;
+  const int rc = spline_eval(bur, R->n_out, b0, b1, W, 20, 60, dp, [&](int o, double v) { ba[(o - 20) * 64] = v * wow; });
+  if (rc < 0) { R->status = FS_TBC; return; }   // benign race: every writer stores the same value
+
+  const double hzs = 1700000 / 140.0;
+  const double m = pwb_s(ba, 40, 64) / 40.0;
+  double mx = 0.0;
+  for (int i = 0; i < 40; i++) { const double v = ba[i * 64] - m; ba[i * 64] = v; mx = fmax(mx, fabs(v)); }
+  const float lf = (float)mx;
+  const double lv = (double)lf;               // numpy-1: float32 element promoted to float64
+  // np.std(ba)
+  const double m2 = pwb_s(ba, 40, 64) / 40.0;
+  for (int i = 0; i < 40; i++) { const double d = ba[i * 64] - m2; tt[i * 64] = d * d; }
+  const double sd = sqrt(pwb_s(tt, 40, 64) / 40.0);
+  double p0 = 0.0, p1 = 0.0;
+  float out_level = lf;
+  if (((lv / hzs) > 30) || (sd / hzs) < 3) {
+    out_level = 0.0f;
+  } else {
+    // zero crossings: offsets stored in tt (in order), group in a bit mask
+    uint64_t tag = 0;
+    int cnt = 0, nF = 0, nT = 0;
+    int bi = 0;
+    while (bi < 40) {
+      if (fabs(ba[bi * 64]) > lv * .6) {
+        double zc;
+        if (calczc_s(ba, 40, bi, 0.0, 10, 64, &zc) == 0) {
+          double off = zc - ((floor(zc / 4) * 4) - 1);
+          if (off > 3.5) off -= 4;
+          const bool pos = ba[bi * 64] > 0;
+          tt[cnt * 64] = off;
+          if (pos) { tag |= (1ull << cnt); nT++; } else nF++;
+          cnt++;
+          bi = (int)zc;
+        }
+      }
+      bi += 1;
+    }
+    if (!(nF < 3 || nT < 3)) {
+      // mean of each group's [1:-1] (np.array of the list, pairwise sum)
+      double gF[40], gT[40];
+      int kF = 0, kT = 0;
+      for (int k = 0; k < cnt; k++) {
+        if ((tag >> k) & 1) gT[kT++] = tt[k * 64];
+        else gF[kF++] = tt[k * 64];
+      }
+      const double mF = pw_sum(gF + 1, kF - 2) / (double)(kF - 2);
+      const double mT = pw_sum(gT + 1, kT - 2) / (double)(kT - 2);
+      if (l % 2) { p0 = 2 - mT; p1 = 2 - mF; }
+      else { p0 = 2 - mF; p1 = 2 - mT; }
+    }
+  }
+  lvl[l] = out_level;
+  pv0[l] = p0;
+  pv1[l] = p1;
+}
+
+// Per-read part of refine_linelocs_burst (lddecode_core.py:1112-1133) and, on
+// the second pass, apply_offsets (:1161-1162, 1184-1186).  grid: n_reads x 64.
+extern "C" __global__ __launch_bounds__(64) void ldg_k_burst_field(FieldRec* __restrict__ recs,
+                                                                   double* __restrict__ lines,
+                                                                   float* __restrict__ blevel, SysConst C,
+                                                                   int pass) {
+  __shared__ double s_c0[MAX_LINES], s_c1[MAX_LINES], s_tmp[MAX_LINES];
+  const int lane = threadIdx.x;
+  const int slot = blockIdx.x;
+  FieldRec* R = recs + slot;
+  if (R->status != FS_PENDING || lane != 0) return;
+  const int nl = R->nlines;
+  double* LN = lines + (int64_t)slot * LINES_STRIDE;
+  const double* li = LN + (pass == 0 ? LL2 : LL3) * MAX_LINES;
+  double* lo = LN + (pass == 0 ? LL3 : LL4) * MAX_LINES;
+  const double* pv0 = LN + PAVG0 * MAX_LINES;
+  const double* pv1 = LN + PAVG1 * MAX_LINES;
+  float* lvl = blevel + (int64_t)slot * MAX_LINES;
+  int nc = 0;
+  for (int l = 0; l < nl; l++)
+    if (pv0[l] != 0 || pv1[l] != 0) { s_c0[nc] = pv0[l]; s_c1[nc] = pv1[l]; nc++; }
+  const double m0 = np_median(s_c0, nc, s_tmp);
+  const double m1 = np_median(s_c1, nc, s_tmp);
+  const int g = (fabs(m0) < fabs(m1)) ? 0 : 1;
+  const double* adj = g ? pv1 : pv0;
+  for (int l = g; l < nl; l += 2) lvl[l] = -lvl[l];
+  const double K = C.freq / ((4.0 * 315.0) / 88.0);
+  for (int l = 0; l < nl; l++) {
+    double v = li[l];
+    if (fabs(adj[l]) > 2) lvl[l] = 0.0f;
+    else v -= adj[l] * K * 1;
+    lo[l] = v;
+  }
+  for (int l = 2; l < nl - 1; l++)
+    if (lvl[l] == 0.0f) lo[l] = (lo[l - 1] + lo[l + 1]) / 2;
+  R->burst_group = g;
+  if (pass == 1) {
+    const double shift = (90 + 1.5) * (3.141592653589793 / 180);
+    const double c = (shift - 8) * K;
+    double* lf = LN + LLF * MAX_LINES;
+    for (int l = 0; l < nl; l++) lf[l] = (lo[l] + 0) + c;
+  }
+}
+
+// Final resample of 'demod' (lineoffset 1 NTSC / 3 PAL, wow) to uint16 .tbc
+// lines (lddecode_core.py:1135-1159 NTSC, :1023-1035 PAL).
+// grid: n_reads * LINE_GROUPS workgroups of 64 threads; lane = output row.
+extern "C" __global__ __launch_bounds__(64) void ldg_k_final_lines(
+    const double* __restrict__ video, int64_t vread_stride, int64_t vchan_stride, SysConst C,
+    FieldRec* __restrict__ recs, const double* __restrict__ lines, const float* __restrict__ blevel,
+    double* __restrict__ scratch, uint16_t* __restrict__ pic, int64_t pic_stride) {
+  const int lane = threadIdx.x;
+  const int slot = blockIdx.x / LINE_GROUPS;
+  const int grp = blockIdx.x % LINE_GROUPS;
+  FieldRec* R = recs + slot;
+  if (R->status != FS_PENDING) return;
+  const int row = grp * 64 + lane;
+  const int lc = R->linecount;
+  if (row >= lc) return;
+  const int loff = (C.system == 1) ? 3 : 1;
+  const int l = row + loff;
+  const double* lf = lines + (int64_t)slot * LINES_STRIDE + LLF * MAX_LINES;
+  const double* dm = video + (int64_t)slot * vread_stride + (int64_t)CH_DEMOD * vchan_stride;
+  double* dp = scratch + (((int64_t)slot * LINE_GROUPS + grp) * SPL_MAXN) * 64 + lane;
+  const int W = C.outlinelen;
+  uint16_t* out = pic + (int64_t)slot * pic_stride + (int64_t)row * W;
+  const double b0 = lf[l], b1 = lf[l + 1];
+  const double wow = (b1 - b0) / (double)C.linelen;
+  const bool pal = C.system == 1;
+  const double scale_ = pal ? (double)(0xd300 - 0x0100) / (100 - C.vsync_ire)
+                            : (double)(0xc800 - 0x0400) / (100 - C.vsync_ire);
+  const double base = pal ? 256.0 : 1024.0;
+  const int rc = spline_eval(dm, R->n_out, b0, b1, W, 0, W, dp, [&](int o, double v) {
+    double red = ((v * wow) - C.ire0) / C.hz_ire;
+    red -= C.vsync_ire;
+    double x = (red * scale_) + base;
+    if (x != x) x = 0.0;
+    x = fmin(fmax(x, 0.0), 65535.0) + 0.5;
+    out[o] = (uint16_t)x;
+  });
+  if (rc < 0) { R->status = FS_TBC; return; }
+  if (!pal && row >= 1 && row < lc - 1) {
+    const float bl = blevel[(int64_t)slot * MAX_LINES + row];
+    const double hzs = 1700000 / 140.0;
+    out[0] = bl > 0 ? 16384 : 32768;
+    const double clevel = (1 / 1.45) / hzs;
+    out[1] = (uint16_t)(327.67 * clevel * fabs((double)bl));
+  }
+}
+
+// Mark reads still pending after the whole chain as valid.
+extern "C" __global__ void ldg_k_finish(FieldRec* __restrict__ recs, int n) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n && recs[i].status == FS_PENDING) recs[i].status = FS_VALID;
+}
+
+// ---------------------------------------------------------------------------
+// downscale_audio (lddecode_core.py:431-484) for n fields.  grid: n x 256.
+extern "C" __global__ __launch_bounds__(256) void ldg_k_audio_ds(
+    const int32_t* __restrict__ slots, const double* __restrict__ offsets, const FieldRec* __restrict__ recs,
+    const double* __restrict__ lines, const double* __restrict__ audio2, int64_t a2read_stride,
+    int64_t a2chan_stride, SysConst C, int16_t* __restrict__ pcm, int64_t pcm_stride, int32_t* __restrict__ counts,
+    double* __restrict__ next_off, int32_t* __restrict__ err) {
+  const int f = blockIdx.x;
+  const int slot = slots[f];
+  const FieldRec* R = recs + slot;
+  const int lc = R->linecount, nl = R->nlines;
+  const double* lf = lines + (int64_t)slot * LINES_STRIDE + LLF * MAX_LINES;
+  const double* aL = audio2 + (int64_t)slot * a2read_stride;
+  const double* aR = aL + a2chan_stride;
+  const int64_t na = R->n_out > 0 ? ((R->n_out - 1) / AUDIO_DIV1 + 1) / AUDIO_DIV2 : 0;
+  const double frametime = (C.line_period * lc) / 1000000;
+  const double gap = 1 / 48000.0;
+  const double start = offsets[f];
+  const double stop = frametime + gap;
+  const int64_t len = (int64_t)ceil((stop - start) / gap);
+  const double t1 = start + gap;
+  const double dl = t1 - start;
+  auto tick = [&](int64_t i) { return i == 0 ? start : (i == 1 ? t1 : start + (double)i * dl); };
+  int16_t* out = pcm + (int64_t)f * pcm_stride;
+  for (int64_t i = threadIdx.x; i < len - 1; i += blockDim.x) {
+    const double t = tick(i);
+    const double ln = ((t * 1000000) / C.line_period) + 1;
+    const int64_t il = (int64_t)ln;
+    if (il < 0 || il >= nl) { atomicOr(err + f, 1); continue; }
+    const double cur = lf[il];
+    const double nxt = (il + 1 < nl) ? lf[il + 1] : cur + C.linelen;
+    double pos = cur;
+    pos += (nxt - cur) * (ln - floor(ln));
+    const double swow = ((nxt - cur) / C.linelen);
+    const double loc = pos / 64;
+    int64_t ai;
+    if (!py_index((int64_t)loc, na, ai)) { atomicOr(err + f, 1); continue; }
+    double left = aL[ai], right = aR[ai];
+    left *= swow; right *= swow;
+    left -= C.audio_lfreq; right -= C.audio_rfreq;
+    double ol = rint(left * 32767 / 150000), orr = rint(right * 32767 / 150000);
+    ol = fmin(fmax(ol, -32766.0), 32766.0);
+    orr = fmin(fmax(orr, -32766.0), 32766.0);
+    out[2 * i] = (int16_t)ol;
+    out[2 * i + 1] = (int16_t)orr;
+  }
+  if (threadIdx.x == 0) {
+    counts[f] = (int32_t)(len - 1);
+    next_off[f] = tick(len - 1) - frametime;
+  }
+}
+
+// Framer.formatoutput: grid (n_frames, frame_lines) x 256.
+extern "C" __global__ __launch_bounds__(256) void ldg_k_frames(const int32_t* __restrict__ top,
+                                                               const int32_t* __restrict__ bot,
+                                                               const FieldRec* __restrict__ recs,
+                                                               const uint16_t* __restrict__ pic, int64_t pic_stride,
+                                                               SysConst C, uint16_t* __restrict__ out) {
+  const int f = blockIdx.x;
+  const int row = blockIdx.y;
+  const int W = C.outlinelen;
+  const int ts = top[f], bs = bot[f];
+  const int lt = recs[ts].linecount, lb = recs[bs].linecount;
+  const int lc = ((lt < lb) ? lt : lb) * 2;
+  uint16_t* dst = out + ((int64_t)f * C.frame_lines + row) * W;
+  const uint16_t* src = nullptr;
+  if (row < lc) src = pic + (int64_t)((row & 1) ? bs : ts) * pic_stride + (int64_t)(row >> 1) * W;
+  else if (row == lc) src = pic + (int64_t)((lt >= lb) ? ts : bs) * pic_stride + (int64_t)(lc >> 1) * W;
+  for (int x = threadIdx.x; x < W; x += blockDim.x) dst[x] = src ? src[x] : 0;
+}
+
+// ---------------------------------------------------------------------------
+// PAL pilot refine (FieldPAL.refine_linelocs_pilot, lddecode_core.py:962-1021).
+// Per line (lane): zero crossings of the flipped (demod - demod_05) 4.7 us
+// window before the line location; offsets to scratch.  Per read: median of
+// all kept offsets -> target phase; per-line median adjustment.
+namespace {
+constexpr int PILOT_MAX = 64;
+__device__ __forceinline__ double* pilot_base(double* scratch, int slot) {
+  return scratch + (int64_t)slot * LINE_GROUPS * SPL_MAXN * 64;
+}
+}  // namespace
+
+extern "C" __global__ __launch_bounds__(64) void ldg_k_pilot_lines(const double* __restrict__ video,
+                                                                   int64_t vread_stride, int64_t vchan_stride,
+                                                                   SysConst C, FieldRec* __restrict__ recs,
+                                                                   double* __restrict__ lines,
+                                                                   double* __restrict__ scratch) {
+  const int lane = threadIdx.x;
+  const int slot = blockIdx.x / LINE_GROUPS;
+  const int grp = blockIdx.x % LINE_GROUPS;
+  FieldRec* R = recs + slot;
+  if (R->status != FS_PENDING) return;
+  const int l = grp * 64 + lane;
+  const int nl = R->nlines;
+  if (l >= nl) return;
+  const double* ll = lines + (int64_t)slot * LINES_STRIDE + LL2 * MAX_LINES;
+  const double* dm = video + (int64_t)slot * vread_stride + (int64_t)CH_DEMOD * vchan_stride;
+  const double* d5 = video + (int64_t)slot * vread_stride + (int64_t)CH_05 * vchan_stride;
+  const int64_t len = R->n_out;
+  double* P = pilot_base(scratch, slot);
+  double* offs = P + (int64_t)l * PILOT_MAX;
+  double* meta = P + (int64_t)MAX_LINES * PILOT_MAX;    // [count, keep, median] per line
+  int64_t a, b;
+  py_slice(py_int(ll[l] - 4.7 * C.freq), py_int(ll[l]), len, a, b);
+  const int pn = (int)(b > a ? b - a : 0);
+  double pil[256];
+  const int pm = pn < 256 ? pn : 256;
+  for (int i = 0; i < pm; i++) pil[i] = dm[b - 1 - i] - d5[b - 1 - i];   // np.flip
+  double adjfreq = C.freq;
+  if (l > 1) adjfreq /= (ll[l] - ll[l - 1]) / (double)C.linelen;
+  int cnt = 0, i = 0;
+  while (i < pn) {
+    if (inrange(pil[i], -300000, -100000)) {
+      double zc;
+      if (calczc(pil, pm, (double)i, 0.0, 10, &zc) == 0) {
+        const double zcp = zc / (adjfreq / 3.75);
+        if (cnt < PILOT_MAX) offs[cnt] = zcp - floor(zcp);
+        cnt++;
+        i = (int)(zc + 1);
+      }
+    }
+    i += 1;
+  }
+  if (cnt > PILOT_MAX) cnt = PILOT_MAX;
+  // offsets[l][1:-1] for l >= 2 (len(offsets dict) >= 3); kept in alloffsets if i >= 11
+  int keep = 0;
+  double med = 0.0;
+  if (l >= 2) {
+    const int k = cnt >= 2 ? cnt - 2 : 0;
+    for (int q = 0; q < k; q++) offs[q] = offs[q + 1];
+    cnt = k;
+    keep = (i >= 11) ? 1 : 0;
+    if (cnt > 0) {
+      double tmp[PILOT_MAX];
+      med = np_median(offs, cnt, tmp);
+    }
+  } else {
+    cnt = 0;
+  }
+  meta[3 * l + 0] = cnt;
+  meta[3 * l + 1] = keep;
+  meta[3 * l + 2] = med;
+}
+
+extern "C" __global__ __launch_bounds__(256) void ldg_k_pilot_field(FieldRec* __restrict__ recs,
+                                                                    double* __restrict__ lines, SysConst C,
+                                                                    double* __restrict__ scratch) {
+  __shared__ double s_all[8192];
+  __shared__ int s_n;
+  const int tid = threadIdx.x;
+  const int slot = blockIdx.x;
+  FieldRec* R = recs + slot;
+  if (R->status != FS_PENDING) return;
+  const int nl = R->nlines;
+  double* P = pilot_base(scratch, slot);
+  const double* meta = P + (int64_t)MAX_LINES * PILOT_MAX;
+  if (tid == 0) {
+    int n = 0;
+    for (int l = 0; l < nl; l++) {
+      if (!meta[3 * l + 1]) continue;
+      const int c = (int)meta[3 * l + 0];
+      for (int q = 0; q < c && n < 8192; q++) s_all[n++] = P[(int64_t)l * PILOT_MAX + q];
+    }
+    s_n = n;
+  }
+  __syncthreads();
+  const int n = s_n;
+  int np2 = 1;
+  while (np2 < n) np2 <<= 1;
+  for (int k = n + tid; k < np2; k += 256) s_all[k] = __builtin_inf();
+  __syncthreads();
+  if (n > 1) block_bitonic_sort(s_all, np2, tid, 256);
+  if (tid != 0) return;
+  const double med = sorted_median(s_all, n);
+  const double tgt = inrange(med, 0.25, 0.75) ? .5 : 0;
+  const double* ll = lines + (int64_t)slot * LINES_STRIDE + LL2 * MAX_LINES;
+  double* lf = lines + (int64_t)slot * LINES_STRIDE + LLF * MAX_LINES;
+  for (int l = 0; l < nl; l++) {
+    double v = ll[l];
+    if (meta[3 * l + 0] > 0) v += (tgt - meta[3 * l + 2]) * (C.freq / 3.75) * .25;
+    lf[l] = v;
+  }
+}

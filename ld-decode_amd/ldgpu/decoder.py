@@ -1,0 +1,341 @@
+"""GPU decode driver: the reference Framer / readfield / readframe / findframe
+control flow (lddecode_core.py:1193-1378, lddecode.py:39-107) over batched,
+speculative field decodes on the GPU.
+
+Why speculation: every field read starts where the previous field's sync
+analysis says (``nextsample = readsample + nextfieldoffset``,
+lddecode_core.py:1204) and uses the MTF level of the previous frame's VBI
+(:1300-1309), and the demod of a read depends on its own overlap-save block
+grid.  To keep the GPU busy, the driver predicts the next B read starts and
+MTF levels, decodes them all in one ``ldg_decode_reads`` call, then replays
+the reference control flow on the returned per-field records.  A read the
+replay asks for that is not in the batch (a misprediction) ends the batch at
+the last completed frame; the next batch restarts from that frame's
+checkpoint.  Results are therefore exactly those of the sequential chain.
+
+Audio offsets (:1289, :484) are a scalar recurrence computed here with the
+reference's own numpy arithmetic; the per-sample audio resampling runs on the
+GPU for all fields of a batch at once.
+"""
+import time
+
+import numpy as np
+
+from . import native
+from .formats import FMT_LDS, FMT_R30, FMT_S16, FMT_U8, bytes_for_samples, samples_in_bytes
+from .rfparams import RFTables
+
+READLEN = 1000000
+BLOCKLEN, BLOCKCUT, BLOCKSTEP = 16384, 1024, 15328
+
+
+class Miss(Exception):
+    """The replay needs a read that the current batch does not hold."""
+
+    def __init__(self, key):
+        super().__init__(key)
+        self.key = key
+
+
+class ReferenceCrash(RuntimeError):
+    """The reference decoder would have raised (uncaught) here."""
+
+
+def read_geometry(start):
+    """Blocks of RFDecode.demod(start, 1e6) (lddecode_core.py:374-385): (s0, end, last block start)."""
+    end = int(start + READLEN) + 1
+    s0 = int(start - BLOCKCUT) if start > BLOCKCUT else 0
+    nb = -(-(end - s0) // BLOCKSTEP)
+    return s0, end, s0 + (nb - 1) * BLOCKSTEP
+
+
+def loader_tell(fmt, sample, nbytes):
+    """File position after loader(infile, sample, 16384) (lddutils.py:131-229) -- fd.tell()."""
+    if fmt == FMT_U8:
+        start, need = sample, BLOCKLEN
+    elif fmt == FMT_S16:
+        start, need = 2 * sample, 2 * BLOCKLEN
+    elif fmt == FMT_R30:
+        start, need = (sample // 3) * 4, int(np.ceil(BLOCKLEN * 3 / 4) * 4) + 4
+    else:
+        start, need = (sample // 4) * 5, int(np.ceil(BLOCKLEN * 5 // 4)) + 5
+    return start + max(0, min(need, nbytes - start))
+
+
+class GPUField:
+    """Field-like view of one decoded read (attributes of lddecode_core.Field)."""
+
+    __slots__ = ('info', 'slot', 'readsample', 'mtf_level', 'audio_offset', 'valid', 'istop', 'linecount',
+                 'nextfieldoffset', 'npeaks', 'nvsync', 'vbi', 'linecode', 'tbcstart', 'status',
+                 'audio_next_offset', 'nextsample', 'dsaudio_used')
+
+    def __init__(self, info, slot, readsample, mtf, audio_offset, sysp, frametime_lines):
+        self.info, self.slot, self.readsample, self.mtf_level = info, slot, readsample, mtf
+        self.audio_offset = audio_offset
+        self.status = info.status
+        self.valid = info.status == native.FS_VALID
+        self.istop = bool(info.istop) if self.valid else None
+        self.linecount = info.linecount
+        self.nextfieldoffset = info.nextfieldoffset
+        self.npeaks, self.nvsync = info.npeaks, info.nvsync
+        self.tbcstart = info.tbcstart
+        self.dsaudio_used = False
+        if self.valid:
+            def v(x):
+                return None if x == native.VBI_NONE else int(x)
+            self.vbi = {'minutes': v(info.vbi_minutes), 'seconds': v(info.vbi_seconds),
+                        'clvframe': v(info.vbi_clvframe), 'framenr': v(info.vbi_framenr),
+                        'statuscode': None, 'status': v(info.vbi_status), 'isclv': bool(info.vbi_isclv)}
+            self.linecode = {str(sysp.codelines[q]): ([int(x) for x in info.linecode[q]] if info.linecode_ok[q] else None)
+                             for q in range(3)}
+            # downscale_audio's returned next offset (lddecode_core.py:432-437,484)
+            frametime = (sysp.line_period * self.linecount) / 1000000
+            gap = 1 / 48000.0
+            ticks = np.arange(audio_offset, frametime + gap, gap, dtype=np.double)
+            self.audio_next_offset = ticks[-1] - frametime
+        else:
+            self.vbi = None
+            self.linecode = None
+            self.audio_next_offset = audio_offset
+
+    def record(self):
+        rec = {'readsample': int(self.readsample), 'nextsample': int(self.nextsample), 'valid': bool(self.valid),
+               'mtf_level': float(self.mtf_level)}
+        if self.valid:
+            rec.update({'istop': bool(self.istop), 'linecount': int(self.linecount),
+                        'nextfieldoffset': int(self.nextfieldoffset), 'vbi': dict(self.vbi),
+                        'linecode': dict(self.linecode)})
+        return rec
+
+
+class FrameOut:
+    __slots__ = ('top', 'bottom', 'audio_fields', 'vbi', 'nextsample', 'fields', 'index')
+
+    def __init__(self, **kw):
+        for k, v in kw.items():
+            setattr(self, k, v)
+
+
+class GPUDecoder:
+    """Decode a capture to .tbc frames / .pcm / per-frame metadata on one GPU."""
+
+    def __init__(self, system='NTSC', device=0, batch=32, log=None):
+        self.rf = RFTables(system)
+        self.sysp = self.rf.system
+        self.batch = batch
+        self.ctx = native.Context(system, device, max_reads=batch, max_frames=batch)
+        self.ctx.set_filters(self.rf.params(), self.rf.tables)
+        self.log = log or (lambda *a: None)
+        self.stats = {'batches': 0, 'reads': 0, 'reads_used': 0, 'gpu_s': 0.0}
+        self.cap_bytes = None
+
+    # ---- capture ---------------------------------------------------------------
+    def set_capture(self, data, fmt, device_ptr=None, nsamples=None):
+        """Whole capture resident in HBM (data: bytes/ndarray, or a device pointer)."""
+        if device_ptr is None:
+            buf = np.frombuffer(data, dtype=np.uint8) if not isinstance(data, np.ndarray) else data.view(np.uint8)
+            nbytes = buf.size
+            nsamples = samples_in_bytes(fmt, nbytes)
+            self.ctx.set_capture(buf, nsamples, fmt, 0)
+        else:
+            nbytes = bytes_for_samples(fmt, nsamples)
+            self.ctx.set_capture(None, nsamples, fmt, 0, device_ptr=device_ptr)
+        self.fmt, self.cap_bytes, self.cap_nsamples = fmt, nbytes, nsamples
+
+    # ---- speculation -------------------------------------------------------------
+    def _predict(self, lead, hist, n):
+        """Batch keys: the exact `lead` keys, then predicted (start, mtf) continuation.
+
+        Starts: NTSC fields repeat exactly every 3 frames (6 fields = 4,004,000
+        samples at 40 MSPS), PAL every frame (1,600,000), so r[k] = r[k-P] + D;
+        before enough history, nominal field spacing.  MTF: the lead's level for
+        the rest of the current frame, then 1 - framenr/1e4 with CAV frame
+        numbers advancing by one per frame (lddecode_core.py:1300-1306).
+        """
+        out = list(lead)
+        starts = list(hist) + [k[0] for k in out]
+        P, D = (6, 4004000) if self.sysp.name == 'NTSC' else (2, 1600000)
+        field_nom = int(round(self.rf.freq_hz / self.sysp.fps / 2))
+        mtf_cur = lead[-1][1]
+        cav = self.last_framenr is not None and not self.last_isclv
+        j = len(lead)
+        while len(out) < n:
+            nxt = starts[-P] + D if len(starts) > P else starts[-1] + field_nom
+            if cav and j >= 2:
+                mtf = 1 - ((self.last_framenr + j // 2) / 10000)
+                if mtf < 0:
+                    mtf = 0
+            else:
+                mtf = mtf_cur
+            out.append((int(nxt), mtf))
+            starts.append(int(nxt))
+            j += 1
+        return out[:n]
+
+    def _run_batch(self, keys):
+        t0 = time.perf_counter()
+        starts = [k[0] for k in keys]
+        mtfs = [k[1] for k in keys]
+        infos = self.ctx.decode_reads(starts, mtfs)
+        self.stats['gpu_s'] += time.perf_counter() - t0
+        self.stats['batches'] += 1
+        self.stats['reads'] += len(keys)
+        self.cache = {k: (i, infos[i]) for i, k in enumerate(keys)}
+        self.requested = []
+
+    # ---- reference control flow --------------------------------------------------
+    def _get(self, readsample, mtf, audio_offset):
+        key = (int(readsample), mtf)
+        self.requested.append(key)
+        hit = self.cache.get(key)
+        if hit is None:
+            raise Miss(key)
+        slot, info = hit
+        if info.status == native.FS_CRASH:
+            raise ReferenceCrash('reference would raise at read %d' % readsample)
+        return GPUField(info, slot, int(readsample), mtf, audio_offset, self.sysp, None)
+
+    def readfield(self, sample):
+        """lddecode_core.py:1194-1223."""
+        readsample = sample
+        while True:
+            f = self._get(readsample, self.mtf_level, self.audio_offset)
+            self.last_read = readsample
+            if f.status == native.FS_EOF:
+                return None, None, None
+            nextsample = readsample + f.nextfieldoffset
+            if not f.valid:
+                if f.npeaks < 100:
+                    nextsample = readsample + (self.rf.freq_hz * 10)
+                elif f.nvsync == 0:
+                    nextsample = readsample + (self.rf.freq_hz * 1)
+            f.nextsample = nextsample
+            self.field_log.append(f)
+            if not f.valid:
+                readsample = nextsample
+            else:
+                return f, readsample, nextsample
+
+    def mergevbi(self, fields):
+        merged = dict(fields[0].vbi)
+        for k in merged:
+            if fields[1].vbi[k] is not None:
+                merged[k] = fields[1].vbi[k]
+        if merged['seconds'] is not None:
+            fps = self.sysp.clvfps
+            merged['framenr'] = merged['minutes'] * 60 * fps + merged['seconds'] * fps + merged['clvframe']
+        return merged
+
+    def readframe(self, sample, firstframe=False):
+        """lddecode_core.py:1254-1311 (formatoutput/audio deferred to the batch flush)."""
+        fieldcount = 0
+        fields = [None, None]
+        audio = []
+        f = None
+        while fieldcount < 2:
+            f, readsample, nextsample = self.readfield(sample)
+            if f is not None:
+                if f.istop:
+                    fields[0] = f
+                else:
+                    fields[1] = f
+                if f.istop == self.sysp.topfirst:
+                    fieldcount = 1
+                elif fieldcount == 1:
+                    fieldcount = 2
+                if fieldcount or not firstframe:
+                    audio.append(f)
+            elif readsample is None:
+                return None
+            sample = nextsample
+        if len(audio):
+            self.audio_offset = f.audio_next_offset
+        vbi = self.mergevbi(fields)
+        self.vbi = vbi
+        self.last_isclv = bool(f.vbi['isclv'])
+        if f.vbi['framenr'] is not None:
+            self.last_framenr = f.vbi['framenr']
+        if not f.vbi['isclv'] and f.vbi['framenr'] is not None:
+            newmtf = 1 - (f.vbi['framenr'] / 10000)
+            if newmtf < 0:
+                newmtf = 0
+            oldmtf = self.mtf_level
+            self.mtf_level = newmtf
+            if np.abs(newmtf - oldmtf) > .1:
+                return self.readframe(sample, firstframe)
+        return FrameOut(top=fields[0], bottom=fields[1], audio_fields=audio, vbi=vbi, nextsample=sample)
+
+    # ---- main loop (lddecode.py:39-107) ------------------------------------------
+    def _tell(self):
+        if self.last_read is None:
+            return 0
+        return loader_tell(self.fmt, read_geometry(self.last_read)[2], self.cap_bytes)
+
+    def decode(self, start_frame=0, length=None, sink=None):
+        """Decode frames; sink(frame_u16, pcm_i16, meta) per frame.  Returns the number of frames."""
+        spf = self.rf.samples_per_frame
+        bpf = spf * 5 // 4                     # (sic) 10-bit packing assumed, lddecode.py:42
+        size = self.cap_bytes
+        if (size // bpf - start_frame) < 2:
+            raise ValueError('start frame is past end of file')
+        num_frames = length if length is not None else size // bpf - start_frame
+        self.mtf_level, self.audio_offset = 1, 0
+        self.last_framenr, self.last_isclv, self.last_read = None, False, None
+        nextsample = start_frame * spf
+        done = 0
+        hist = []
+        lead = []
+        W, H = self.sysp.outlinelen, self.sysp.frame_lines
+        while done < num_frames and self._tell() + bpf * 1.05 <= size:
+            keys = self._predict(lead or [(int(nextsample), self.mtf_level)], hist, self.batch)
+            self._run_batch(keys)
+            frames, lead = [], []
+            eof = False
+            while done + len(frames) < num_frames and self._tell() + bpf * 1.05 <= size:
+                cp = (nextsample, self.mtf_level, self.audio_offset, self.last_framenr, self.last_isclv,
+                      self.last_read)
+                mark = len(self.requested)
+                self.field_log = []
+                try:
+                    fr = self.readframe(nextsample, (done + len(frames)) == 0)
+                except Miss:
+                    lead = list(dict.fromkeys(self.requested[mark:]))
+                    (nextsample, self.mtf_level, self.audio_offset, self.last_framenr, self.last_isclv,
+                     self.last_read) = cp
+                    break
+                if fr is None:
+                    eof = True
+                    break
+                fr.fields = [x.record() for x in self.field_log]
+                fr.index = done + len(frames)
+                frames.append(fr)
+                nextsample = fr.nextsample
+                hist = (hist + [x.readsample for x in self.field_log])[-16:]
+            self._flush(frames, W, H, sink)
+            done += len(frames)
+            self.stats['reads_used'] += sum(len(f.fields) for f in frames)
+            if eof or (not frames and not lead):
+                break
+            if not frames and len(lead) >= self.batch:
+                raise RuntimeError('batch of %d reads cannot hold one frame' % self.batch)
+        return done
+
+    def _flush(self, frames, W, H, sink):
+        if not frames:
+            return
+        tops = [f.top.slot for f in frames]
+        bots = [f.bottom.slot for f in frames]
+        pics = self.ctx.assemble_frames(tops, bots, W, H)
+        af = [(fr_i, x) for fr_i, fr in enumerate(frames) for x in fr.audio_fields]
+        if af:
+            pcm, counts, _ = self.ctx.field_audio([x.slot for _, x in af], [x.audio_offset for _, x in af])
+        per_frame = [[] for _ in frames]
+        for j, (fr_i, x) in enumerate(af):
+            if counts[j] < 0:
+                raise ReferenceCrash('audio index error (reference: field invalid)')
+            per_frame[fr_i].append(pcm[j, :2 * counts[j]])
+        for i, fr in enumerate(frames):
+            audio = np.concatenate(per_frame[i]) if per_frame[i] else np.zeros(0, dtype=np.int16)
+            meta = {'frame': fr.index, 'vbi': dict(fr.vbi), 'nextsample': int(fr.nextsample), 'fields': fr.fields}
+            if sink:
+                sink(pics[i], audio, meta)

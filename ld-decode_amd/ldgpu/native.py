@@ -1,0 +1,207 @@
+"""ctypes binding of libldgpu.so (include/ldgpu.h).
+
+The library is built in-tree (``ld-decode_amd/ldgpu/libldgpu.so``) by
+``__graft_entry__.build()``.  There is no CPU fallback: if the library or a
+GPU is missing, ``load()`` / ``Context`` raise.
+"""
+import ctypes as C
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, 'libldgpu.so')
+
+LDG_OK = 0
+FS_VALID, FS_NO_VSYNC, FS_SHORT, FS_LINELOCS, FS_TBC, FS_EOF, FS_CRASH, FS_PENDING = range(8)
+VBI_NONE = -2147483648
+MAX_VSYNCS = 16
+
+EXPORTS = ['ldg_create', 'ldg_destroy', 'ldg_last_error', 'ldg_set_filters', 'ldg_set_capture',
+           'ldg_decode_reads', 'ldg_field_audio', 'ldg_assemble_frames', 'ldg_debug_read',
+           'ldg_comb_ntsc', 'ldg_comb_reset', 'ldg_version', 'ldg_device_count']
+
+
+class FieldInfo(C.Structure):
+    _fields_ = [('status', C.c_int32), ('npeaks', C.c_int32), ('nvsync', C.c_int32), ('istop', C.c_int32),
+                ('linecount', C.c_int32), ('nlines', C.c_int32), ('n_out', C.c_int64),
+                ('nextfieldoffset', C.c_int64), ('tbcstart', C.c_int64), ('med_hsync', C.c_double),
+                ('hsync_tol', C.c_double), ('vsync', (C.c_int32 * 3) * MAX_VSYNCS),
+                ('linecode', (C.c_int32 * 6) * 3), ('linecode_ok', C.c_int32 * 3),
+                ('vbi_minutes', C.c_int32), ('vbi_seconds', C.c_int32), ('vbi_clvframe', C.c_int32),
+                ('vbi_framenr', C.c_int32), ('vbi_status', C.c_int32), ('vbi_isclv', C.c_int32),
+                ('burst_group', C.c_int32), ('pad_', C.c_int32)]
+
+
+class Config(C.Structure):
+    _fields_ = [('system', C.c_int32), ('device', C.c_int32), ('max_reads', C.c_int32),
+                ('max_frames', C.c_int32)]
+
+
+class Params(C.Structure):
+    _fields_ = [('freq_hz', C.c_double), ('freq', C.c_double), ('ire0', C.c_double), ('hz_ire', C.c_double),
+                ('vsync_ire', C.c_double), ('sync_lo', C.c_double), ('sync_hi', C.c_double),
+                ('freq_arf', C.c_double), ('audio_lowfreq', C.c_double), ('audio_lfreq', C.c_double),
+                ('audio_rfreq', C.c_double), ('line_period', C.c_double), ('fsc_mhz', C.c_double),
+                ('linelen', C.c_int32), ('outlinelen', C.c_int32), ('frame_lines', C.c_int32),
+                ('audio_lo0', C.c_int32), ('codelines', C.c_int32 * 3), ('pad_', C.c_int32)]
+
+
+_DP = C.POINTER(C.c_double)
+
+
+class Filters(C.Structure):
+    _fields_ = [(k, _DP) for k in ('rfvideo', 'mtf', 'fvideo', 'fvideo05', 'fvideoburst', 'fvideopilot', 'fpsync',
+                                   'audio_lfilt', 'audio_rfilt', 'audio_lpf2', 'mtf_logabs', 'mtf_arg')]
+
+
+_lib = None
+
+
+def load(path=LIB_PATH):
+    """Load libldgpu.so and declare its signatures (no device access)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise RuntimeError('libldgpu.so not built (%s); run __graft_entry__.build()' % path)
+    lib = C.CDLL(path)
+    vp = C.c_void_p
+    lib.ldg_create.argtypes = [C.POINTER(Config), C.POINTER(vp)]
+    lib.ldg_destroy.argtypes = [vp]
+    lib.ldg_last_error.argtypes = [vp]
+    lib.ldg_last_error.restype = C.c_char_p
+    lib.ldg_set_filters.argtypes = [vp, C.POINTER(Params), C.POINTER(Filters)]
+    lib.ldg_set_capture.argtypes = [vp, vp, C.c_int64, C.c_int, C.c_int64, C.c_int]
+    lib.ldg_decode_reads.argtypes = [vp, C.c_int, C.POINTER(C.c_int64), C.POINTER(C.c_double), C.POINTER(FieldInfo)]
+    lib.ldg_field_audio.argtypes = [vp, C.c_int, C.POINTER(C.c_int32), C.POINTER(C.c_double),
+                                    C.POINTER(C.c_int16), C.c_int64, C.POINTER(C.c_int32), C.POINTER(C.c_double)]
+    lib.ldg_assemble_frames.argtypes = [vp, C.c_int, C.POINTER(C.c_int32), C.POINTER(C.c_int32),
+                                        C.POINTER(C.c_uint16), C.c_int]
+    lib.ldg_debug_read.argtypes = [vp, C.c_int, C.c_int, vp, C.c_int64]
+    lib.ldg_debug_read.restype = C.c_int64
+    lib.ldg_comb_ntsc.argtypes = [vp, C.c_int, vp, vp, C.c_int]
+    lib.ldg_comb_reset.argtypes = [vp]
+    lib.ldg_version.restype = C.c_char_p
+    lib.ldg_device_count.restype = C.c_int
+    _lib = lib
+    return lib
+
+
+def _ptr(a, t=C.c_double):
+    return a.ctypes.data_as(C.POINTER(t))
+
+
+class LDGError(RuntimeError):
+    pass
+
+
+class Context:
+    """One libldgpu context (one GPU).  Owns device memory for ``max_reads`` field reads."""
+
+    def __init__(self, system='NTSC', device=0, max_reads=32, max_frames=None):
+        self.lib = load()
+        if self.lib.ldg_device_count() <= 0:
+            raise LDGError('no HIP device visible: the ldgpu decode path needs an MI355X (no CPU fallback)')
+        cfg = Config(1 if system == 'PAL' else 0, device, max_reads, max_frames or max_reads)
+        h = C.c_void_p()
+        rc = self.lib.ldg_create(C.byref(cfg), C.byref(h))
+        if rc != LDG_OK:
+            raise LDGError('ldg_create failed (%d)' % rc)
+        self.h = h
+        self.system = system
+        self.max_reads = max_reads
+        self.max_frames = max_frames or max_reads
+        self._keep = []
+
+    def _check(self, rc, what):
+        if rc != LDG_OK:
+            raise LDGError('%s failed (%d): %s' % (what, rc, self.lib.ldg_last_error(self.h).decode()))
+
+    def close(self):
+        if self.h:
+            self.lib.ldg_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def set_filters(self, params, tables):
+        """params: dict of ldg_params fields; tables: dict name -> complex128/float64 array."""
+        p = Params()
+        for k, _ in Params._fields_:
+            if k == 'codelines':
+                for i, v in enumerate(params['codelines']):
+                    p.codelines[i] = int(v)
+            elif k != 'pad_':
+                setattr(p, k, params[k])
+        keep = {}
+        f = Filters()
+        for k, _ in Filters._fields_:
+            a = tables.get(k)
+            if a is None:
+                setattr(f, k, C.POINTER(C.c_double)())
+                continue
+            if np.iscomplexobj(a):
+                a = np.ascontiguousarray(a, dtype=np.complex128).view(np.float64)
+            else:
+                a = np.ascontiguousarray(a, dtype=np.float64)
+            keep[k] = a
+            setattr(f, k, _ptr(a))
+        self._check(self.lib.ldg_set_filters(self.h, C.byref(p), C.byref(f)), 'ldg_set_filters')
+        self.params = params
+
+    def set_capture(self, raw, nsamples, fmt, first_sample=0, device_ptr=None):
+        if device_ptr is not None:
+            rc = self.lib.ldg_set_capture(self.h, C.c_void_p(device_ptr), nsamples, fmt, first_sample, 1)
+        else:
+            buf = np.frombuffer(raw, dtype=np.uint8) if not isinstance(raw, np.ndarray) else raw.view(np.uint8)
+            buf = np.ascontiguousarray(buf)
+            rc = self.lib.ldg_set_capture(self.h, buf.ctypes.data_as(C.c_void_p), nsamples, fmt, first_sample, 0)
+        self._check(rc, 'ldg_set_capture')
+
+    def decode_reads(self, starts, mtfs):
+        n = len(starts)
+        s = np.ascontiguousarray(starts, dtype=np.int64)
+        m = np.ascontiguousarray(mtfs, dtype=np.float64)
+        info = (FieldInfo * n)()
+        self._check(self.lib.ldg_decode_reads(self.h, n, _ptr(s, C.c_int64), _ptr(m), info), 'ldg_decode_reads')
+        return list(info)
+
+    def field_audio(self, slots, offsets):
+        n = len(slots)
+        stride = 2048
+        pcm = np.zeros((max(n, 1), stride), dtype=np.int16)
+        counts = np.zeros(max(n, 1), dtype=np.int32)
+        nxt = np.zeros(max(n, 1), dtype=np.float64)
+        sl = np.ascontiguousarray(slots, dtype=np.int32)
+        of = np.ascontiguousarray(offsets, dtype=np.float64)
+        self._check(self.lib.ldg_field_audio(self.h, n, _ptr(sl, C.c_int32), _ptr(of), _ptr(pcm, C.c_int16), stride,
+                                             _ptr(counts, C.c_int32), _ptr(nxt)), 'ldg_field_audio')
+        return pcm[:n], counts[:n], nxt[:n]
+
+    def assemble_frames(self, tops, bottoms, W, H):
+        n = len(tops)
+        out = np.zeros((max(n, 1), H * W), dtype=np.uint16)
+        t = np.ascontiguousarray(tops, dtype=np.int32)
+        b = np.ascontiguousarray(bottoms, dtype=np.int32)
+        self._check(self.lib.ldg_assemble_frames(self.h, n, _ptr(t, C.c_int32), _ptr(b, C.c_int32),
+                                                 _ptr(out, C.c_uint16), 0), 'ldg_assemble_frames')
+        return out[:n]
+
+    def debug(self, slot, what, dtype, count):
+        a = np.zeros(count, dtype=dtype)
+        rc = self.lib.ldg_debug_read(self.h, slot, what, a.ctypes.data_as(C.c_void_p), a.nbytes)
+        if rc < 0:
+            raise LDGError('ldg_debug_read(%d,%d) -> %d' % (slot, what, rc))
+        return a[:rc // a.itemsize]
+
+    def comb_ntsc(self, frames):
+        f = np.ascontiguousarray(frames, dtype=np.uint16).reshape(-1, 525 * 910)
+        out = np.zeros((f.shape[0], 480 * 744 * 3), dtype=np.uint16)
+        self._check(self.lib.ldg_comb_ntsc(self.h, f.shape[0], f.ctypes.data_as(C.c_void_p),
+                                           out.ctypes.data_as(C.c_void_p), 0), 'ldg_comb_ntsc')
+        return out
