@@ -1,0 +1,169 @@
+"""Benchmark: RF Msamples/s and fields/s of the MI355X decode path (BASELINE.json metric).
+
+    python bench.py [--gpus N --steps K --warmup W]
+    (N > 1: torch.distributed.run, one rank per GPU, weak scaling)
+
+Workload (BASELINE.json configs[1]): 60 s of synthetic NTSC CAV RF, 40 MSPS,
+8-bit, per GPU, synthesised on the GPU straight into HBM (same signal model as
+ldgpu/synth.py).  One step = the full reference decode of that capture:
+RF -> demod -> TBC -> .tbc frames (+ .pcm audio), every frame of the 60 s,
+with the .tbc frames assembled in HBM.  Ranks decode independent captures
+(fields shard by capture; no data-path collective).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, 'ld-decode_amd'))
+
+import numpy as np  # noqa: E402
+
+NTSC_TBC_BYTES_PER_SAMPLE = 955500 / 1334667
+NTSC_PCM_BYTES_PER_SAMPLE = 0.0048
+BYTES_PER_SAMPLE = {0: 1.0, 1: 2.0, 2: 4 / 3, 3: 1.25}
+HBM_PEAK_GBS = 8000.0
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--gpus', type=int, default=1)
+    ap.add_argument('--steps', type=int, default=2)
+    ap.add_argument('--warmup', type=int, default=1)
+    ap.add_argument('--seconds', type=float, default=60.0)
+    ap.add_argument('--batch', type=int, default=64)
+    ap.add_argument('--fmt', type=int, default=0)
+    ap.add_argument('--cpu-seconds', type=float, default=0.3, help='oracle baseline sample (seconds of RF)')
+    ap.add_argument('--no-cpu', action='store_true')
+    return ap.parse_args()
+
+
+def cpu_baseline(seconds):
+    """Oracle (numpy restatement of lddecode_core.py) on a bounded sample, one core."""
+    from threadpoolctl import threadpool_limits
+    from ldgpu.synth import make_capture
+    from oracle.capture import FMT_U8
+    from oracle.framer import decode_capture
+    data = make_capture(int(40e6 * seconds), 'u8', seed=99)
+    with threadpool_limits(limits=1):
+        t0 = time.perf_counter()
+        frames, pcm, meta = decode_capture(data, FMT_U8)
+        dt = time.perf_counter() - t0
+    consumed = meta[-1]['nextsample'] if meta else 0
+    return {'value': consumed / dt / 1e6, 'unit': 'RF Msamples/s', 'cores': 1, 'kind': 'port',
+            'sample': '%.2f s synthetic NTSC CAV u8 RF -> %d frames through the oracle (numpy restatement of '
+                      'lddecode_core.py), %.1f s wall on 1 core' % (seconds, len(frames), dt),
+            'fields_per_s': 2 * len(frames) / dt}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get('WORLD_SIZE', '1'))
+    rank = int(os.environ.get('RANK', '0'))
+    local = int(os.environ.get('LOCAL_RANK', '0'))
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as tdist
+        torch.cuda.set_device(local)
+        tdist.init_process_group('nccl' if torch.cuda.is_available() else 'gloo')
+        dist = tdist
+
+    from ldgpu.decoder import GPUDecoder
+    dec = GPUDecoder(system='NTSC', device=local, batch=args.batch)
+    nsamp = int(40e6 * args.seconds)
+    t0 = time.perf_counter()
+    # per-rank capture: its own CAV picture-number range and noise seed
+    dec.ctx.synth(nsamp, fmt=args.fmt, first_frame=1 + 2000 * (rank % 39), seed=20181015 + rank)
+    dec.use_resident_capture(args.fmt, nsamp)
+    synth_s = time.perf_counter() - t0
+
+    def step():
+        return dec.decode(sink=None)
+
+    for _ in range(args.warmup):
+        nfr = step()
+
+    def barrier():
+        if dist is not None:
+            import torch
+            torch.cuda.synchronize()
+            dist.barrier()
+
+    dec.ctx.profile(True)
+    barrier()
+    t0 = time.perf_counter()
+    frames = 0
+    consumed = 0
+    for _ in range(args.steps):
+        frames += step()
+        consumed += dec.last_meta['nextsample']
+    barrier()
+    dt = time.perf_counter() - t0
+    stats = dec.ctx.profile_stats()
+    dec.ctx.profile(False)
+    # sanity on the full-size output: consecutive CAV picture numbers, all frames present
+    nrs = dec.frame_numbers
+    consecutive = all(b == a + 1 for a, b in zip(nrs, nrs[1:]))
+
+    if dist is not None:
+        import torch
+        t = torch.tensor([dt, float(frames), float(consumed)], dtype=torch.float64, device='cuda')
+        tmax = t.clone()
+        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        dt_max, frames_all, consumed_all = float(tmax[0]), float(t[1]), float(t[2])
+    else:
+        dt_max, frames_all, consumed_all = dt, float(frames), float(consumed)
+
+    if rank != 0:
+        if dist is not None:
+            dist.destroy_process_group()
+        return
+
+    msps = consumed_all / dt_max / 1e6
+    fields_s = 2 * frames_all / dt_max
+    # roofline of the dominant kernel (HIP events around each launch, on the library's stream)
+    dom = max(stats.items(), key=lambda kv: kv[1][1]) if stats else ('demod', (1, float('nan')))
+    dom_name, (dom_launches, dom_ms) = dom
+    avg_ms = dom_ms / max(dom_launches, 1)
+    bps = BYTES_PER_SAMPLE[args.fmt] + NTSC_TBC_BYTES_PER_SAMPLE + NTSC_PCM_BYTES_PER_SAMPLE
+    units_per_launch = (consumed / max(args.steps, 1)) / max(dom_launches / max(args.steps, 1), 1)
+    achieved = bps * units_per_launch / (avg_ms * 1e-3) / 1e9
+    traffic = None
+    pmc = os.path.join(ROOT, 'profiles', 'pmc_traffic.json')
+    if os.path.exists(pmc):
+        try:
+            traffic = json.load(open(pmc)).get(dom_name)
+        except Exception:
+            traffic = None
+    cpu = None if args.no_cpu else cpu_baseline(args.cpu_seconds)
+    line = {
+        'metric': 'RF Msamples/s (40 MSPS NTSC, full RF->.tbc decode)', 'value': round(msps, 3),
+        'unit': 'RF Msamples/s', 'n_gpus': world, 'steps': args.steps, 'warmup': args.warmup,
+        'ms_per_step': round(dt_max / args.steps * 1e3, 3), 'higher_is_better': True, 'scaling': 'weak',
+        'vs_baseline': None, 'dtype': 'f64', 'data': 'synthetic (GPU-synthesised NTSC CAV RF, u8)',
+        'config': {'workload': '%g s NTSC CAV, 40 MSPS 8-bit RF per GPU: RF->demod->TBC->.tbc+.pcm' % args.seconds,
+                   'frames_per_step': frames // max(args.steps, 1), 'batch_reads': args.batch,
+                   'parallelism': 'capture-sharded x%d' % world},
+        'fields_per_s': round(fields_s, 1), 'realtime_x': round(msps / 40.0, 2),
+        'roofline': {'bound': 'hbm', 'kernel': dom_name, 'achieved': round(achieved, 4), 'peak': HBM_PEAK_GBS,
+                     'unit': 'GB/s', 'frac': achieved / HBM_PEAK_GBS, 'traffic': traffic,
+                     'avg_launch_ms': round(avg_ms, 4), 'launches': dom_launches,
+                     'algorithmic_bytes_per_sample': round(bps, 4)},
+        'kernels_ms': {k: round(v[1], 3) for k, v in sorted(stats.items(), key=lambda kv: -kv[1][1])},
+        'cpu_baseline': cpu,
+        'checks': {'cav_framenr_consecutive': consecutive, 'synth_s': round(synth_s, 2),
+                   'reads_decoded': dec.stats['reads'], 'reads_used': dec.stats['reads_used'],
+                   'batches': dec.stats['batches']},
+    }
+    print(json.dumps(line), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == '__main__':
+    main()

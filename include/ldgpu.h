@@ -162,6 +162,35 @@ int64_t ldg_debug_read(ldg_ctx* ctx, int slot, int what, void* dst, int64_t cap)
 int ldg_comb_ntsc(ldg_ctx* ctx, int n, const uint16_t* frames, uint16_t* rgb_out, int io_is_device);
 int ldg_comb_reset(ldg_ctx* ctx);
 
+/* ---- in-library kernel timing (HIP events on the context's stream) ------------- */
+typedef struct ldg_kernel_stat {
+  char name[48];
+  int64_t launches;
+  double total_ms; /* sum of per-launch event durations */
+} ldg_kernel_stat;
+/* on != 0: record a start/stop event pair around every kernel launch (resets stats). */
+int ldg_profile_enable(ldg_ctx* ctx, int on);
+/* Copy up to max per-kernel records; returns the number of kernels recorded. */
+int ldg_profile_read(ldg_ctx* ctx, ldg_kernel_stat* out, int max);
+
+/* ---- benchmark / test tooling (not a reference interface) ----------------------
+ * Synthesise an NTSC LaserDisc RF capture directly into this context's HBM
+ * capture buffer (same signal model as ldgpu/synth.py), then make it the
+ * current capture (first_sample 0).  fir: 63 band-limit taps; emph: b0, b1, a1
+ * of the pre-emphasis IIR; codes: 3 Philips code words per frame. */
+typedef struct ldg_synth_params {
+  int32_t fmt;          /* LDG_FMT_* of the generated capture */
+  int32_t pad_;
+  int64_t nsamples;
+  uint64_t seed;
+  double noise;         /* Gaussian sigma relative to the unit video carrier */
+  double start_line;    /* capture starts this many lines into frame 0 */
+} ldg_synth_params;
+int ldg_synth_capture(ldg_ctx* ctx, const ldg_synth_params* p, const double* fir63, const double* emph,
+                      const uint32_t* codes, int64_t ncodeframes);
+/* Copy nbytes of the resident capture starting at byte offset to host dst. */
+int64_t ldg_capture_download(ldg_ctx* ctx, void* dst, int64_t offset, int64_t nbytes);
+
 /* Library / device identification. */
 const char* ldg_version(void);
 int ldg_device_count(void);

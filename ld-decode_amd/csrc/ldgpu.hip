@@ -3,4 +3,5 @@
 #include "field.hip"
 #include "tbc.hip"
 #include "comb.hip"
+#include "synth.hip"
 #include "abi.inc"

@@ -142,6 +142,11 @@ class GPUDecoder:
             self.ctx.set_capture(None, nsamples, fmt, 0, device_ptr=device_ptr)
         self.fmt, self.cap_bytes, self.cap_nsamples = fmt, nbytes, nsamples
 
+    def use_resident_capture(self, fmt, nsamples):
+        """The capture already lives in this context's HBM (e.g. Context.synth)."""
+        self.fmt, self.cap_nsamples = fmt, nsamples
+        self.cap_bytes = bytes_for_samples(fmt, nsamples)
+
     # ---- speculation -------------------------------------------------------------
     def _predict(self, lead, hist, n):
         """Batch keys: the exact `lead` keys, then predicted (start, mtf) continuation.
@@ -281,6 +286,7 @@ class GPUDecoder:
         num_frames = length if length is not None else size // bpf - start_frame
         self.mtf_level, self.audio_offset = 1, 0
         self.last_framenr, self.last_isclv, self.last_read = None, False, None
+        self.frame_numbers, self.pcm_samples, self.last_meta = [], 0, None
         nextsample = start_frame * spf
         done = 0
         hist = []
@@ -325,7 +331,12 @@ class GPUDecoder:
             return
         tops = [f.top.slot for f in frames]
         bots = [f.bottom.slot for f in frames]
-        pics = self.ctx.assemble_frames(tops, bots, W, H)
+        if sink is None:
+            # benchmark mode: .tbc frames stay in HBM
+            self.ctx.assemble_frames_device(tops, bots)
+            pics = None
+        else:
+            pics = self.ctx.assemble_frames(tops, bots, W, H)
         af = [(fr_i, x) for fr_i, fr in enumerate(frames) for x in fr.audio_fields]
         if af:
             pcm, counts, _ = self.ctx.field_audio([x.slot for _, x in af], [x.audio_offset for _, x in af])
@@ -337,5 +348,9 @@ class GPUDecoder:
         for i, fr in enumerate(frames):
             audio = np.concatenate(per_frame[i]) if per_frame[i] else np.zeros(0, dtype=np.int16)
             meta = {'frame': fr.index, 'vbi': dict(fr.vbi), 'nextsample': int(fr.nextsample), 'fields': fr.fields}
+            self.last_meta = meta
+            self.frame_numbers.append(fr.vbi['framenr'])
             if sink:
                 sink(pics[i], audio, meta)
+            else:
+                self.pcm_samples += audio.size

@@ -19,7 +19,8 @@ MAX_VSYNCS = 16
 
 EXPORTS = ['ldg_create', 'ldg_destroy', 'ldg_last_error', 'ldg_set_filters', 'ldg_set_capture',
            'ldg_decode_reads', 'ldg_field_audio', 'ldg_assemble_frames', 'ldg_debug_read',
-           'ldg_comb_ntsc', 'ldg_comb_reset', 'ldg_version', 'ldg_device_count']
+           'ldg_comb_ntsc', 'ldg_comb_reset', 'ldg_version', 'ldg_device_count', 'ldg_profile_enable',
+           'ldg_profile_read', 'ldg_synth_capture', 'ldg_capture_download']
 
 
 class FieldInfo(C.Structure):
@@ -45,6 +46,15 @@ class Params(C.Structure):
                 ('audio_rfreq', C.c_double), ('line_period', C.c_double), ('fsc_mhz', C.c_double),
                 ('linelen', C.c_int32), ('outlinelen', C.c_int32), ('frame_lines', C.c_int32),
                 ('audio_lo0', C.c_int32), ('codelines', C.c_int32 * 3), ('pad_', C.c_int32)]
+
+
+class KernelStat(C.Structure):
+    _fields_ = [('name', C.c_char * 48), ('launches', C.c_int64), ('total_ms', C.c_double)]
+
+
+class SynthParams(C.Structure):
+    _fields_ = [('fmt', C.c_int32), ('pad_', C.c_int32), ('nsamples', C.c_int64), ('seed', C.c_uint64),
+                ('noise', C.c_double), ('start_line', C.c_double)]
 
 
 _DP = C.POINTER(C.c_double)
@@ -82,6 +92,12 @@ def load(path=LIB_PATH):
     lib.ldg_debug_read.restype = C.c_int64
     lib.ldg_comb_ntsc.argtypes = [vp, C.c_int, vp, vp, C.c_int]
     lib.ldg_comb_reset.argtypes = [vp]
+    lib.ldg_profile_enable.argtypes = [vp, C.c_int]
+    lib.ldg_profile_read.argtypes = [vp, C.POINTER(KernelStat), C.c_int]
+    lib.ldg_synth_capture.argtypes = [vp, C.POINTER(SynthParams), C.POINTER(C.c_double), C.POINTER(C.c_double),
+                                      C.POINTER(C.c_uint32), C.c_int64]
+    lib.ldg_capture_download.argtypes = [vp, vp, C.c_int64, C.c_int64]
+    lib.ldg_capture_download.restype = C.c_int64
     lib.ldg_version.restype = C.c_char_p
     lib.ldg_device_count.restype = C.c_int
     _lib = lib
@@ -183,6 +199,14 @@ class Context:
                                              _ptr(counts, C.c_int32), _ptr(nxt)), 'ldg_field_audio')
         return pcm[:n], counts[:n], nxt[:n]
 
+    def assemble_frames_device(self, tops, bottoms):
+        """Assemble frames into the context's device frame buffer (no host copy)."""
+        n = len(tops)
+        t = np.ascontiguousarray(tops, dtype=np.int32)
+        b = np.ascontiguousarray(bottoms, dtype=np.int32)
+        self._check(self.lib.ldg_assemble_frames(self.h, n, _ptr(t, C.c_int32), _ptr(b, C.c_int32),
+                                                 C.POINTER(C.c_uint16)(), 1), 'ldg_assemble_frames')
+
     def assemble_frames(self, tops, bottoms, W, H):
         n = len(tops)
         out = np.zeros((max(n, 1), H * W), dtype=np.uint16)
@@ -205,3 +229,34 @@ class Context:
         self._check(self.lib.ldg_comb_ntsc(self.h, f.shape[0], f.ctypes.data_as(C.c_void_p),
                                            out.ctypes.data_as(C.c_void_p), 0), 'ldg_comb_ntsc')
         return out
+
+    # ---- profiling / tooling -------------------------------------------------------
+    def profile(self, on=True):
+        self._check(self.lib.ldg_profile_enable(self.h, 1 if on else 0), 'ldg_profile_enable')
+
+    def profile_stats(self):
+        arr = (KernelStat * 64)()
+        n = self.lib.ldg_profile_read(self.h, arr, 64)
+        return {arr[i].name.decode(): (int(arr[i].launches), float(arr[i].total_ms)) for i in range(min(n, 64))}
+
+    def synth(self, nsamples, fmt=0, first_frame=1, clv=False, seed=20181015, noise=0.02, start_line=100):
+        """Generate a synthetic NTSC capture straight into this context's HBM capture buffer."""
+        import scipy.signal as sps
+        from .synth import NTSC, FrameCodes, emphasis_filter, FS
+        fir = np.ascontiguousarray(sps.firwin(63, 4.4e6 / (FS / 2)), dtype=np.float64)
+        b, a = emphasis_filter(NTSC)
+        emph = np.array([b[0], b[1], a[1]], dtype=np.float64)
+        spl = FS * NTSC['line_us'] / 1e6
+        nframes = int((nsamples / spl + start_line) // 525) + 2
+        fc = FrameCodes(first_frame, clv, 30)
+        codes = np.array([fc.codes(k) for k in range(nframes)], dtype=np.uint32).reshape(-1)
+        p = SynthParams(fmt, 0, nsamples, seed, noise, start_line)
+        self._check(self.lib.ldg_synth_capture(self.h, C.byref(p), _ptr(fir), _ptr(emph), _ptr(codes, C.c_uint32),
+                                               nframes), 'ldg_synth_capture')
+
+    def capture_download(self, offset, nbytes):
+        a = np.zeros(nbytes, dtype=np.uint8)
+        n = self.lib.ldg_capture_download(self.h, a.ctypes.data_as(C.c_void_p), offset, nbytes)
+        if n < 0:
+            raise LDGError('ldg_capture_download -> %d' % n)
+        return a[:n]

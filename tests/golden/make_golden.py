@@ -1,0 +1,75 @@
+"""Regenerate tests/golden/*.json from the oracle (CPU) on deterministic synthetic captures.
+
+    python tests/golden/make_golden.py
+
+Each fixture holds: the generator settings, SHA-256 of the capture bytes,
+per-frame SHA-256 of the .tbc frame and .pcm audio, the per-frame metadata
+(VBI + per-field records), and a few small per-stage vectors of the first
+valid field read (demod channels around a sync pulse, final line locations).
+"""
+import hashlib
+import json
+import os
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, 'ld-decode_amd'))
+
+import numpy as np  # noqa: E402
+
+from ldgpu.synth import make_capture  # noqa: E402
+from oracle.capture import FMT_BY_EXT, Capture  # noqa: E402
+from oracle.demod import RFDemod  # noqa: E402
+from oracle.field import FieldNTSC  # noqa: E402
+from oracle.framer import decode_capture  # noqa: E402
+
+CASES = {
+    'ntsc_cav_u8_0p2s': dict(seconds=0.2, fmt='u8', system='NTSC', kw={}),
+    'ntsc_clv_u8_0p2s': dict(seconds=0.2, fmt='u8', system='NTSC', kw={'clv': True, 'first_frame': 5399}),
+    'ntsc_cav_r30_0p15s': dict(seconds=0.15, fmt='r30', system='NTSC', kw={'seed': 7}),
+    'ntsc_cav_lds_0p15s': dict(seconds=0.15, fmt='lds', system='NTSC', kw={'seed': 8}),
+}
+
+
+def sha(b):
+    return hashlib.sha256(bytes(b)).hexdigest()
+
+
+def build_capture(case):
+    c = CASES[case]
+    return make_capture(int(40e6 * c['seconds']), c['fmt'], system=c['system'], **c['kw'])
+
+
+def make(case):
+    c = CASES[case]
+    data = build_capture(case)
+    fmt = FMT_BY_EXT[c['fmt']]
+    frames, pcm, meta = decode_capture(data, fmt, system=c['system'])
+    out = {'case': case, 'settings': {k: v for k, v in c.items()}, 'capture_sha256': sha(data),
+           'frames': [{'tbc_sha256': sha(f.tobytes()), 'pcm_sha256': sha(a.tobytes()), 'pcm_len': int(a.size),
+                       'meta': m} for f, a, m in zip(frames, pcm, meta)]}
+    # per-stage vectors of the first valid field
+    rf = RFDemod(system=c['system'])
+    cap = Capture(data, fmt)
+    first = next(fr for m in meta for fr in m['fields'] if fr['valid'])
+    raw = rf.demod(cap, first['readsample'], 1000000, first['mtf_level'])
+    f = FieldNTSC(rf, raw, 0, audio_offset=0)
+    p = int(f.peaklist[20])
+    out['stage'] = {'readsample': first['readsample'], 'mtf_level': first['mtf_level'], 'peak20': p,
+                    'demod': raw[0]['demod'][p - 8:p + 8].tolist(),
+                    'demod_05': raw[0]['demod_05'][p - 8:p + 8].tolist(),
+                    'demod_sync': raw[0]['demod_sync'][p - 8:p + 8].tolist(),
+                    'demod_burst': raw[0]['demod_burst'][p - 8:p + 8].tolist(),
+                    'linelocs': [float(x) for x in f.linelocs[:12]],
+                    'burstlevel': [float(x) for x in f.burstlevel[:12]]}
+    path = os.path.join(HERE, case + '.json')
+    with open(path, 'w') as fh:
+        json.dump(out, fh, indent=1)
+    print('wrote', path, len(frames), 'frames')
+
+
+if __name__ == '__main__':
+    for case in (sys.argv[1:] or CASES):
+        make(case)
