@@ -92,7 +92,7 @@ typedef struct ldg_ctx ldg_ctx;
 typedef struct ldg_config {
   int32_t system;    /* LDG_SYSTEM_NTSC / LDG_SYSTEM_PAL      */
   int32_t device;    /* HIP device ordinal                     */
-  int32_t max_reads; /* field reads per ldg_decode_reads call  */
+  int32_t max_reads; /* device read slots (and max reads per ldg_decode_reads call) */
   int32_t max_frames;/* frames per ldg_assemble_frames call    */
 } ldg_config;
 
@@ -133,12 +133,15 @@ int ldg_set_capture(ldg_ctx* ctx, const void* data, int64_t nsamples, int fmt, i
 
 /* Demodulate and analyse n field reads: read i starts at read_starts[i] (the
  * `start` argument of RFDecode.demod, readlen 1,000,000) with MTF level
- * mtf[i].  Fills info[i]; pictures stay on the device, addressed by i. */
-int ldg_decode_reads(ldg_ctx* ctx, int n, const int64_t* read_starts, const double* mtf,
+ * mtf[i] and is stored in device slot slots[i] (0 <= slot < max_reads,
+ * distinct; slots == NULL means slot i).  Fills info[i].  A slot keeps its
+ * read (demod channels, line locations, .tbc lines) until it is reused, so a
+ * host may cache reads across calls. */
+int ldg_decode_reads(ldg_ctx* ctx, int n, const int64_t* read_starts, const double* mtf, const int32_t* slots,
                      ldg_field_info* info);
 
-/* 48 kHz audio for fields (slots of the last ldg_decode_reads) with the given
- * starting time offsets.  pcm receives, per field, 2*count int16 samples at
+/* 48 kHz audio for fields in the given slots with the given starting time
+ * offsets.  pcm receives, per field, 2*count int16 samples at
  * pcm + i * pcm_stride; counts[i], next_offsets[i] are returned. */
 int ldg_field_audio(ldg_ctx* ctx, int n, const int32_t* slots, const double* offsets, int16_t* pcm,
                     int64_t pcm_stride, int32_t* counts, double* next_offsets);
@@ -148,7 +151,7 @@ int ldg_field_audio(ldg_ctx* ctx, int n, const int32_t* slots, const double* off
 int ldg_assemble_frames(ldg_ctx* ctx, int n, const int32_t* top_slots, const int32_t* bottom_slots,
                         uint16_t* out, int out_is_device);
 
-/* Debug / parity access to per-read device arrays of the last ldg_decode_reads.
+/* Debug / parity access to the per-read device arrays of a live slot.
  * what: 0..4 demod channels (demod, demod_05, demod_sync, demod_burst, demod_pilot)
  *       [float64, n_out]; 10,11: audio_left/right after phase 2 [float64];
  *       20..24: linelocs1, linelocs2, linelocs3, linelocs4, final linelocs [float64];

@@ -114,7 +114,7 @@ __device__ __forceinline__ void merge_filtered(double* re, double* im, const dou
 
 // grid: n_reads * MAX_BLOCKS_PER_READ workgroups of 1024 threads.
 extern "C" __global__ __launch_bounds__(1024) void ldg_k_demod(
-    const ReadDesc* __restrict__ reads, const uint8_t* __restrict__ cap, int64_t cap_first, int64_t cap_nsamp,
+    const int32_t* __restrict__ smap, const ReadDesc* __restrict__ reads, const uint8_t* __restrict__ cap, int64_t cap_first, int64_t cap_nsamp,
     int fmt, const double2* __restrict__ tw, const double2* __restrict__ rf_filt,
     const double2* __restrict__ g_video, const double2* __restrict__ g_05, const double2* __restrict__ g_burst,
     const double2* __restrict__ g_pilot, const double2* __restrict__ g_psync,
@@ -124,7 +124,7 @@ extern "C" __global__ __launch_bounds__(1024) void ldg_k_demod(
   __shared__ double s_re[LDSN];
   __shared__ double s_im[LDSN];
   const int tid = threadIdx.x;
-  const int slot = blockIdx.x / MAX_BLOCKS_PER_READ;
+  const int slot = smap[blockIdx.x / MAX_BLOCKS_PER_READ];
   const int b = blockIdx.x % MAX_BLOCKS_PER_READ;
   const ReadDesc rd = reads[slot];
   if (b >= rd.n_blocks) return;
@@ -320,7 +320,7 @@ extern "C" __global__ __launch_bounds__(1024) void ldg_k_demod(
 // times audio_lpf2, 4096-point IFFT, real part / 4.
 // grid: n_reads * 8 * 2 workgroups of 1024 threads.
 extern "C" __global__ __launch_bounds__(1024) void ldg_k_audio2(
-    const ReadDesc* __restrict__ reads, const double2* __restrict__ tw, const double2* __restrict__ lpf2,
+    const int32_t* __restrict__ smap, const ReadDesc* __restrict__ reads, const double2* __restrict__ tw, const double2* __restrict__ lpf2,
     const double* __restrict__ audio1, int64_t aread_stride, int64_t achan_stride,
     double* __restrict__ audio2, int64_t a2read_stride, int64_t a2chan_stride, const int32_t* __restrict__ status) {
   __shared__ double s_re[LDSN];
@@ -328,7 +328,7 @@ extern "C" __global__ __launch_bounds__(1024) void ldg_k_audio2(
   const int tid = threadIdx.x;
   const int ch = blockIdx.x & 1;
   const int j = (blockIdx.x >> 1) & 7;
-  const int slot = blockIdx.x >> 4;
+  const int slot = smap[blockIdx.x >> 4];
   if (status[slot] == FS_EOF) return;
   const ReadDesc rd = reads[slot];
   const int n_in = rd.n_audio, n_out = rd.n_audio2;

@@ -46,14 +46,14 @@ struct SyncView {
 // Sync peaks, hsync median/tolerance, vsyncs and the Field.__init__ branch.
 // grid: n_reads workgroups of 64 threads (one wave).
 extern "C" __global__ __launch_bounds__(64) void ldg_k_sync(
-    const ReadDesc* __restrict__ reads, const double* __restrict__ video, int64_t vread_stride,
+    const int32_t* __restrict__ smap, const ReadDesc* __restrict__ reads, const double* __restrict__ video, int64_t vread_stride,
     int64_t vchan_stride, SysConst C, FieldRec* __restrict__ recs, int32_t* __restrict__ peaks,
     const int32_t* __restrict__ status) {
   __shared__ int32_t s_pk[MAX_PEAKS];
   __shared__ double s_lv[MAX_PEAKS];
   __shared__ double s_tmp[2 * MAX_PEAKS];
   const int lane = threadIdx.x;
-  const int slot = blockIdx.x;
+  const int slot = smap[blockIdx.x];
   FieldRec* R = recs + slot;
   const ReadDesc rd = reads[slot];
   if (lane == 0) R->n_out = rd.n_out;
@@ -76,10 +76,17 @@ extern "C" __global__ __launch_bounds__(64) void ldg_k_sync(
     const int64_t wend = (i + win < len) ? i + win : len;
     double best = -__builtin_inf();
     int64_t bidx = 0x7fffffffffffffffLL;
-    for (int64_t k = i + lane; k < wend; k += 64) {
-      const double v = ds[k];
-      if (v > best) { best = v; bidx = k; }
+    // all of this lane's window loads issued back to back, then a first-occurrence max
+    constexpr int PER = 20;                         // ceil(1280 / 64): PAL window 1280, NTSC 1271
+    double vv[PER];
+#pragma unroll
+    for (int q = 0; q < PER; q++) {
+      const int64_t k = i + lane + 64 * q;
+      vv[q] = (k < wend) ? ds[k] : -__builtin_inf();
     }
+#pragma unroll
+    for (int q = 0; q < PER; q++)
+      if (vv[q] > best) { best = vv[q]; bidx = i + lane + 64 * q; }
     for (int o = 32; o > 0; o >>= 1) {
       const double ov = __shfl_xor(best, o);
       const int64_t oi = __shfl_xor(bidx, o);
@@ -216,7 +223,7 @@ extern "C" __global__ __launch_bounds__(64) void ldg_k_sync(
 // ---------------------------------------------------------------------------
 // compute_linelocs (lddecode_core.py:638-713).  grid: n_reads x 64 threads; lane 0.
 extern "C" __global__ __launch_bounds__(64) void ldg_k_linelocs(
-    const double* __restrict__ video, int64_t vread_stride, int64_t vchan_stride, SysConst C,
+    const int32_t* __restrict__ smap, const double* __restrict__ video, int64_t vread_stride, int64_t vchan_stride, SysConst C,
     FieldRec* __restrict__ recs, const int32_t* __restrict__ peaks, double* __restrict__ lines,
     int8_t* __restrict__ bad) {
   __shared__ double s_key[LINENUM_SPAN];
@@ -224,7 +231,7 @@ extern "C" __global__ __launch_bounds__(64) void ldg_k_linelocs(
   __shared__ uint8_t s_orig[LINENUM_SPAN];
   __shared__ double s_lv[MAX_PEAKS];
   const int lane = threadIdx.x;
-  const int slot = blockIdx.x;
+  const int slot = smap[blockIdx.x];
   FieldRec* R = recs + slot;
   if (R->status != FS_PENDING) return;
   const int np = R->npeaks;
@@ -325,13 +332,13 @@ extern "C" __global__ __launch_bounds__(64) void ldg_k_linelocs(
 // grid: n_reads x 256 threads: per-line crossing searches in parallel, then
 // the sequential bad-line extrapolation and the two end fix-ups on thread 0.
 extern "C" __global__ __launch_bounds__(256) void ldg_k_hsync(
-    const double* __restrict__ video, int64_t vread_stride, int64_t vchan_stride, SysConst C,
+    const int32_t* __restrict__ smap, const double* __restrict__ video, int64_t vread_stride, int64_t vchan_stride, SysConst C,
     FieldRec* __restrict__ recs, double* __restrict__ lines, int8_t* __restrict__ bad) {
   __shared__ double s_v[MAX_LINES];
   __shared__ int8_t s_bad[MAX_LINES];
   __shared__ int s_err;
   const int tid = threadIdx.x;
-  const int slot = blockIdx.x;
+  const int slot = smap[blockIdx.x];
   FieldRec* R = recs + slot;
   if (R->status != FS_PENDING) return;
   const int nl = R->nlines;
@@ -426,12 +433,12 @@ extern "C" __global__ __launch_bounds__(256) void ldg_k_hsync(
 // Philips VBI decode (lddecode_core.py:814-884).  grid: n_reads x 64; lanes 0..2
 // decode one code line each, lane 0 then interprets them.
 extern "C" __global__ __launch_bounds__(64) void ldg_k_philips(
-    const double* __restrict__ video, int64_t vread_stride, int64_t vchan_stride, SysConst C,
+    const int32_t* __restrict__ smap, const double* __restrict__ video, int64_t vread_stride, int64_t vchan_stride, SysConst C,
     FieldRec* __restrict__ recs, const double* __restrict__ lines) {
   __shared__ int32_t s_code[3][6];
   __shared__ int32_t s_ok[3];
   const int lane = threadIdx.x;
-  const int slot = blockIdx.x;
+  const int slot = smap[blockIdx.x];
   FieldRec* R = recs + slot;
   if (R->status != FS_PENDING) return;
   const double* dm = video + (int64_t)slot * vread_stride + (int64_t)CH_DEMOD * vchan_stride;

@@ -129,13 +129,13 @@ __device__ inline int calczc_s(const double* d, int len, int s, double target, i
 // refine_linelocs_burst (lddecode_core.py:1069-1110).
 // grid: n_reads * LINE_GROUPS workgroups of 64 threads; lane = line.
 extern "C" __global__ __launch_bounds__(64) void ldg_k_burst_lines(
-    const double* __restrict__ video, int64_t vread_stride, int64_t vchan_stride, SysConst C,
+    const int32_t* __restrict__ smap, const double* __restrict__ video, int64_t vread_stride, int64_t vchan_stride, SysConst C,
     FieldRec* __restrict__ recs, double* __restrict__ lines, float* __restrict__ blevel,
     double* __restrict__ scratch, int pass) {
   __shared__ double s_ba[40 * 64];
   __shared__ double s_t[40 * 64];
   const int lane = threadIdx.x;
-  const int slot = blockIdx.x / LINE_GROUPS;
+  const int slot = smap[blockIdx.x / LINE_GROUPS];
   const int grp = blockIdx.x % LINE_GROUPS;
   FieldRec* R = recs + slot;
   if (R->status != FS_PENDING) return;
@@ -213,15 +213,17 @@ extern "C" __global__ __launch_bounds__(64) void ldg_k_burst_lines(
 
 // Per-read part of refine_linelocs_burst (lddecode_core.py:1112-1133) and, on
 // the second pass, apply_offsets (:1161-1162, 1184-1186).  grid: n_reads x 64.
-extern "C" __global__ __launch_bounds__(64) void ldg_k_burst_field(FieldRec* __restrict__ recs,
+extern "C" __global__ __launch_bounds__(64) void ldg_k_burst_field(const int32_t* __restrict__ smap,
+                                                                   FieldRec* __restrict__ recs,
                                                                    double* __restrict__ lines,
                                                                    float* __restrict__ blevel, SysConst C,
                                                                    int pass) {
-  __shared__ double s_c0[MAX_LINES], s_c1[MAX_LINES], s_tmp[MAX_LINES];
+  __shared__ double s_c0[512], s_c1[512];
+  __shared__ int s_nc;
   const int lane = threadIdx.x;
-  const int slot = blockIdx.x;
+  const int slot = smap[blockIdx.x];
   FieldRec* R = recs + slot;
-  if (R->status != FS_PENDING || lane != 0) return;
+  if (R->status != FS_PENDING) return;
   const int nl = R->nlines;
   double* LN = lines + (int64_t)slot * LINES_STRIDE;
   const double* li = LN + (pass == 0 ? LL2 : LL3) * MAX_LINES;
@@ -229,11 +231,30 @@ extern "C" __global__ __launch_bounds__(64) void ldg_k_burst_field(FieldRec* __r
   const double* pv0 = LN + PAVG0 * MAX_LINES;
   const double* pv1 = LN + PAVG1 * MAX_LINES;
   float* lvl = blevel + (int64_t)slot * MAX_LINES;
-  int nc = 0;
-  for (int l = 0; l < nl; l++)
-    if (pv0[l] != 0 || pv1[l] != 0) { s_c0[nc] = pv0[l]; s_c1[nc] = pv1[l]; nc++; }
-  const double m0 = np_median(s_c0, nc, s_tmp);
-  const double m1 = np_median(s_c1, nc, s_tmp);
+  // phaseaverages_cut: rows with a nonzero entry, then np.median of each column (wave bitonic sort)
+  if (lane == 0) {
+    int nc = 0;
+    for (int l = 0; l < nl; l++)
+      if (pv0[l] != 0 || pv1[l] != 0) { s_c0[nc] = pv0[l]; s_c1[nc] = pv1[l]; nc++; }
+    s_nc = nc;
+  }
+  __syncthreads();
+  const int nc = s_nc;
+  int np2 = 1;
+  while (np2 < nc) np2 <<= 1;
+  for (int k = nc + lane; k < np2; k += 64) { s_c0[k] = __builtin_inf(); s_c1[k] = __builtin_inf(); }
+  __syncthreads();
+  bool nan0 = false, nan1 = false;
+  for (int k = lane; k < nc; k += 64) { nan0 |= s_c0[k] != s_c0[k]; nan1 |= s_c1[k] != s_c1[k]; }
+  nan0 = __any(nan0);
+  nan1 = __any(nan1);
+  if (nc > 1) {
+    block_bitonic_sort(s_c0, np2, lane, 64);
+    block_bitonic_sort(s_c1, np2, lane, 64);
+  }
+  if (lane != 0) return;
+  const double m0 = nan0 ? __builtin_nan("") : sorted_median(s_c0, nc);
+  const double m1 = nan1 ? __builtin_nan("") : sorted_median(s_c1, nc);
   const int g = (fabs(m0) < fabs(m1)) ? 0 : 1;
   const double* adj = g ? pv1 : pv0;
   for (int l = g; l < nl; l += 2) lvl[l] = -lvl[l];
@@ -259,11 +280,11 @@ extern "C" __global__ __launch_bounds__(64) void ldg_k_burst_field(FieldRec* __r
 // lines (lddecode_core.py:1135-1159 NTSC, :1023-1035 PAL).
 // grid: n_reads * LINE_GROUPS workgroups of 64 threads; lane = output row.
 extern "C" __global__ __launch_bounds__(64) void ldg_k_final_lines(
-    const double* __restrict__ video, int64_t vread_stride, int64_t vchan_stride, SysConst C,
+    const int32_t* __restrict__ smap, const double* __restrict__ video, int64_t vread_stride, int64_t vchan_stride, SysConst C,
     FieldRec* __restrict__ recs, const double* __restrict__ lines, const float* __restrict__ blevel,
     double* __restrict__ scratch, uint16_t* __restrict__ pic, int64_t pic_stride) {
   const int lane = threadIdx.x;
-  const int slot = blockIdx.x / LINE_GROUPS;
+  const int slot = smap[blockIdx.x / LINE_GROUPS];
   const int grp = blockIdx.x % LINE_GROUPS;
   FieldRec* R = recs + slot;
   if (R->status != FS_PENDING) return;
@@ -302,9 +323,9 @@ extern "C" __global__ __launch_bounds__(64) void ldg_k_final_lines(
 }
 
 // Mark reads still pending after the whole chain as valid.
-extern "C" __global__ void ldg_k_finish(FieldRec* __restrict__ recs, int n) {
+extern "C" __global__ void ldg_k_finish(const int32_t* __restrict__ smap, FieldRec* __restrict__ recs, int n) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n && recs[i].status == FS_PENDING) recs[i].status = FS_VALID;
+  if (i < n && recs[smap[i]].status == FS_PENDING) recs[smap[i]].status = FS_VALID;
 }
 
 // ---------------------------------------------------------------------------
@@ -390,13 +411,14 @@ __device__ __forceinline__ double* pilot_base(double* scratch, int slot) {
 }
 }  // namespace
 
-extern "C" __global__ __launch_bounds__(64) void ldg_k_pilot_lines(const double* __restrict__ video,
+extern "C" __global__ __launch_bounds__(64) void ldg_k_pilot_lines(const int32_t* __restrict__ smap,
+                                                                   const double* __restrict__ video,
                                                                    int64_t vread_stride, int64_t vchan_stride,
                                                                    SysConst C, FieldRec* __restrict__ recs,
                                                                    double* __restrict__ lines,
                                                                    double* __restrict__ scratch) {
   const int lane = threadIdx.x;
-  const int slot = blockIdx.x / LINE_GROUPS;
+  const int slot = smap[blockIdx.x / LINE_GROUPS];
   const int grp = blockIdx.x % LINE_GROUPS;
   FieldRec* R = recs + slot;
   if (R->status != FS_PENDING) return;
@@ -452,13 +474,14 @@ extern "C" __global__ __launch_bounds__(64) void ldg_k_pilot_lines(const double*
   meta[3 * l + 2] = med;
 }
 
-extern "C" __global__ __launch_bounds__(256) void ldg_k_pilot_field(FieldRec* __restrict__ recs,
+extern "C" __global__ __launch_bounds__(256) void ldg_k_pilot_field(const int32_t* __restrict__ smap,
+                                                                    FieldRec* __restrict__ recs,
                                                                     double* __restrict__ lines, SysConst C,
                                                                     double* __restrict__ scratch) {
   __shared__ double s_all[8192];
   __shared__ int s_n;
   const int tid = threadIdx.x;
-  const int slot = blockIdx.x;
+  const int slot = smap[blockIdx.x];
   FieldRec* R = recs + slot;
   if (R->status != FS_PENDING) return;
   const int nl = R->nlines;

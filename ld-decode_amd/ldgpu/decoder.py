@@ -117,17 +117,31 @@ class FrameOut:
 
 
 class GPUDecoder:
-    """Decode a capture to .tbc frames / .pcm / per-frame metadata on one GPU."""
+    """Decode a capture to .tbc frames / .pcm / per-frame metadata on one GPU.
 
-    def __init__(self, system='NTSC', device=0, batch=32, log=None):
+    Device reads live in ``capacity`` slots (a read cache).  Each GPU launch
+    decodes up to ``batch`` reads the forward simulator predicts the replay
+    will ask for; the replay (the reference control flow) consumes cached
+    reads, and a miss just triggers the next plan from the last completed
+    frame, re-using every read already decoded.
+    """
+
+    def __init__(self, system='NTSC', device=0, batch=32, capacity=None, log=None):
         self.rf = RFTables(system)
         self.sysp = self.rf.system
         self.batch = batch
-        self.ctx = native.Context(system, device, max_reads=batch, max_frames=batch)
+        self.capacity = capacity or max(2 * batch, batch + 16)
+        self.ctx = native.Context(system, device, max_reads=self.capacity, max_frames=self.capacity)
         self.ctx.set_filters(self.rf.params(), self.rf.tables)
         self.log = log or (lambda *a: None)
-        self.stats = {'batches': 0, 'reads': 0, 'reads_used': 0, 'gpu_s': 0.0}
+        self.stats = {'batches': 0, 'reads': 0, 'reads_used': 0, 'gpu_s': 0.0, 'replay_s': 0.0}
         self.cap_bytes = None
+        self.cache = {}            # (start, mtf) -> (slot, info)
+        self.hints = {}            # start -> absolute next start (start + nextfieldoffset)
+        self._hint_keys = []       # sorted starts with hints
+        P, D = (6, 4004000) if self.sysp.name == 'NTSC' else (2, 1600000)
+        self.period, self.period_samples = P, D          # exact at 40 MSPS: 3 NTSC / 1 PAL frames
+        self.field_nom = int(round(self.rf.freq_hz / self.sysp.fps / 2))
 
     # ---- capture ---------------------------------------------------------------
     def set_capture(self, data, fmt, device_ptr=None, nsamples=None):
@@ -141,52 +155,132 @@ class GPUDecoder:
             nbytes = bytes_for_samples(fmt, nsamples)
             self.ctx.set_capture(None, nsamples, fmt, 0, device_ptr=device_ptr)
         self.fmt, self.cap_bytes, self.cap_nsamples = fmt, nbytes, nsamples
+        self._reset_cache()
 
     def use_resident_capture(self, fmt, nsamples):
         """The capture already lives in this context's HBM (e.g. Context.synth)."""
         self.fmt, self.cap_nsamples = fmt, nsamples
         self.cap_bytes = bytes_for_samples(fmt, nsamples)
+        self._reset_cache()
 
-    # ---- speculation -------------------------------------------------------------
-    def _predict(self, lead, hist, n):
-        """Batch keys: the exact `lead` keys, then predicted (start, mtf) continuation.
+    def _reset_cache(self):
+        self.cache, self.hints, self._hint_keys = {}, {}, []
 
-        Starts: NTSC fields repeat exactly every 3 frames (6 fields = 4,004,000
-        samples at 40 MSPS), PAL every frame (1,600,000), so r[k] = r[k-P] + D;
-        before enough history, nominal field spacing.  MTF: the lead's level for
-        the rest of the current frame, then 1 - framenr/1e4 with CAV frame
-        numbers advancing by one per frame (lddecode_core.py:1300-1306).
-        """
-        out = list(lead)
-        starts = list(hist) + [k[0] for k in out]
-        P, D = (6, 4004000) if self.sysp.name == 'NTSC' else (2, 1600000)
-        field_nom = int(round(self.rf.freq_hz / self.sysp.fps / 2))
-        mtf_cur = lead[-1][1]
-        cav = self.last_framenr is not None and not self.last_isclv
-        j = len(lead)
-        while len(out) < n:
-            nxt = starts[-P] + D if len(starts) > P else starts[-1] + field_nom
-            if cav and j >= 2:
-                mtf = 1 - ((self.last_framenr + j // 2) / 10000)
-                if mtf < 0:
-                    mtf = 0
-            else:
-                mtf = mtf_cur
-            out.append((int(nxt), mtf))
-            starts.append(int(nxt))
-            j += 1
-        return out[:n]
+    # ---- forward simulator (plans the next GPU launch) ---------------------------
+    def _next_known(self, start, info):
+        """readfield's next position for a decoded read (lddecode_core.py:1204-1212)."""
+        nxt = start + info.nextfieldoffset
+        if info.status != native.FS_VALID:
+            if info.npeaks < 100:
+                nxt = start + (self.rf.freq_hz * 10)
+            elif info.nvsync == 0:
+                nxt = start + (self.rf.freq_hz * 1)
+        return nxt
 
-    def _run_batch(self, keys):
+    def _hint(self, start):
+        """Next start predicted from any decoded read within 4096 samples (sync peaks are signal-locked)."""
+        import bisect
+        ks = self._hint_keys
+        i = bisect.bisect_left(ks, start - 4096)
+        best = None
+        while i < len(ks) and ks[i] <= start + 4096:
+            if best is None or abs(ks[i] - start) < abs(best - start):
+                best = ks[i]
+            i += 1
+        return None if best is None else self.hints[best]
+
+    def _plan(self, nextsample, mtf, last_framenr, isclv, firstframe, want, hist):
+        """Simulate the replay from a frame checkpoint; return up to `want` undecoded keys it will need."""
+        new, seen, chain = [], set(), []
+        starts = list(hist)
+        sample, cur_mtf, fr = int(nextsample), mtf, last_framenr
+        prev_top = None
+        steps = 0
+        while len(new) < want and steps < 8 * want:
+            fieldcount = 0
+            last = None
+            while fieldcount < 2 and steps < 8 * want:
+                steps += 1
+                key = (int(sample), cur_mtf)
+                hit = self.cache.get(key)
+                if hit is None and key not in seen:
+                    seen.add(key)
+                    new.append(key)
+                    if len(new) >= want:
+                        return new, chain
+                if hit is not None:
+                    chain.append(key)
+                    info = hit[1]
+                    if info.status == native.FS_EOF or info.status == native.FS_CRASH:
+                        return new, chain
+                    nxt = self._next_known(key[0], info)
+                    valid = info.status == native.FS_VALID
+                    istop = bool(info.istop) if valid else None
+                    fnr = info.vbi_framenr if valid and info.vbi_framenr != native.VBI_NONE else None
+                    clv = bool(info.vbi_isclv) if valid else isclv
+                else:
+                    h = self._hint(key[0])
+                    if h is not None:
+                        nxt = h
+                    elif len(starts) >= self.period:
+                        nxt = starts[-self.period] + self.period_samples
+                    else:
+                        nxt = key[0] + self.field_nom
+                    valid = True
+                    istop = (not prev_top) if prev_top is not None else self.sysp.topfirst
+                    fnr = (fr + 1) if (fr is not None and not isclv) else None
+                    clv = isclv
+                starts.append(key[0])
+                sample = nxt
+                if not valid:
+                    continue
+                prev_top = istop
+                if istop == self.sysp.topfirst:
+                    fieldcount = 1
+                elif fieldcount == 1:
+                    fieldcount = 2
+                last = (fnr, clv)
+            if last is None:
+                break
+            fnr, clv = last
+            isclv = clv
+            if fnr is not None:
+                fr = fnr
+                if not clv:
+                    newmtf = 1 - (fnr / 10000)
+                    if newmtf < 0:
+                        newmtf = 0
+                    cur_mtf = newmtf
+            firstframe = False
+        return new, chain
+
+    def _launch(self, keys, protect):
+        """Decode `keys` into free slots (evicting cache entries not in `protect`)."""
+        used = {v[0] for k, v in self.cache.items() if k in protect}
+        free = [s for s in range(self.capacity) if s not in used]
+        if len(free) < len(keys):
+            keys = keys[:len(free)]
+        if not keys:
+            raise RuntimeError('read cache full (capacity %d)' % self.capacity)
+        for k in [k for k in self.cache if k not in protect]:
+            del self.cache[k]
+        slots = free[:len(keys)]
         t0 = time.perf_counter()
-        starts = [k[0] for k in keys]
-        mtfs = [k[1] for k in keys]
-        infos = self.ctx.decode_reads(starts, mtfs)
+        infos = self.ctx.decode_reads([k[0] for k in keys], [k[1] for k in keys], slots)
         self.stats['gpu_s'] += time.perf_counter() - t0
         self.stats['batches'] += 1
         self.stats['reads'] += len(keys)
-        self.cache = {k: (i, infos[i]) for i, k in enumerate(keys)}
-        self.requested = []
+        import bisect
+        for k, sl, inf in zip(keys, slots, infos):
+            self.cache[k] = (sl, inf)
+            if inf.status in (native.FS_VALID, native.FS_SHORT):
+                if k[0] not in self.hints:
+                    bisect.insort(self._hint_keys, k[0])
+                self.hints[k[0]] = k[0] + inf.nextfieldoffset
+        if len(self._hint_keys) > 4096:           # keep the hint index bounded
+            for s in self._hint_keys[:-2048]:
+                self.hints.pop(s, None)
+            self._hint_keys = self._hint_keys[-2048:]
 
     # ---- reference control flow --------------------------------------------------
     def _get(self, readsample, mtf, audio_offset):
@@ -277,7 +371,9 @@ class GPUDecoder:
         return loader_tell(self.fmt, read_geometry(self.last_read)[2], self.cap_bytes)
 
     def decode(self, start_frame=0, length=None, sink=None):
-        """Decode frames; sink(frame_u16, pcm_i16, meta) per frame.  Returns the number of frames."""
+        """Decode frames; sink(frame_u16, pcm_i16, meta) per frame (None: frames stay in HBM).
+
+        Returns the number of frames decoded."""
         spf = self.rf.samples_per_frame
         bpf = spf * 5 // 4                     # (sic) 10-bit packing assumed, lddecode.py:42
         size = self.cap_bytes
@@ -290,22 +386,23 @@ class GPUDecoder:
         nextsample = start_frame * spf
         done = 0
         hist = []
-        lead = []
         W, H = self.sysp.outlinelen, self.sysp.frame_lines
         while done < num_frames and self._tell() + bpf * 1.05 <= size:
-            keys = self._predict(lead or [(int(nextsample), self.mtf_level)], hist, self.batch)
-            self._run_batch(keys)
-            frames, lead = [], []
+            plan, chain = self._plan(nextsample, self.mtf_level, self.last_framenr, self.last_isclv, done == 0,
+                                     self.batch, hist)
+            if plan:
+                self._launch(plan, set(chain))
+            frames = []
             eof = False
+            t0 = time.perf_counter()
+            self.requested = []
             while done + len(frames) < num_frames and self._tell() + bpf * 1.05 <= size:
                 cp = (nextsample, self.mtf_level, self.audio_offset, self.last_framenr, self.last_isclv,
                       self.last_read)
-                mark = len(self.requested)
                 self.field_log = []
                 try:
                     fr = self.readframe(nextsample, (done + len(frames)) == 0)
                 except Miss:
-                    lead = list(dict.fromkeys(self.requested[mark:]))
                     (nextsample, self.mtf_level, self.audio_offset, self.last_framenr, self.last_isclv,
                      self.last_read) = cp
                     break
@@ -317,13 +414,12 @@ class GPUDecoder:
                 frames.append(fr)
                 nextsample = fr.nextsample
                 hist = (hist + [x.readsample for x in self.field_log])[-16:]
+            self.stats['replay_s'] += time.perf_counter() - t0
             self._flush(frames, W, H, sink)
             done += len(frames)
             self.stats['reads_used'] += sum(len(f.fields) for f in frames)
-            if eof or (not frames and not lead):
+            if eof or (not frames and not plan):
                 break
-            if not frames and len(lead) >= self.batch:
-                raise RuntimeError('batch of %d reads cannot hold one frame' % self.batch)
         return done
 
     def _flush(self, frames, W, H, sink):

@@ -83,7 +83,8 @@ def load(path=LIB_PATH):
     lib.ldg_last_error.restype = C.c_char_p
     lib.ldg_set_filters.argtypes = [vp, C.POINTER(Params), C.POINTER(Filters)]
     lib.ldg_set_capture.argtypes = [vp, vp, C.c_int64, C.c_int, C.c_int64, C.c_int]
-    lib.ldg_decode_reads.argtypes = [vp, C.c_int, C.POINTER(C.c_int64), C.POINTER(C.c_double), C.POINTER(FieldInfo)]
+    lib.ldg_decode_reads.argtypes = [vp, C.c_int, C.POINTER(C.c_int64), C.POINTER(C.c_double),
+                                     C.POINTER(C.c_int32), C.POINTER(FieldInfo)]
     lib.ldg_field_audio.argtypes = [vp, C.c_int, C.POINTER(C.c_int32), C.POINTER(C.c_double),
                                     C.POINTER(C.c_int16), C.c_int64, C.POINTER(C.c_int32), C.POINTER(C.c_double)]
     lib.ldg_assemble_frames.argtypes = [vp, C.c_int, C.POINTER(C.c_int32), C.POINTER(C.c_int32),
@@ -179,12 +180,14 @@ class Context:
             rc = self.lib.ldg_set_capture(self.h, buf.ctypes.data_as(C.c_void_p), nsamples, fmt, first_sample, 0)
         self._check(rc, 'ldg_set_capture')
 
-    def decode_reads(self, starts, mtfs):
+    def decode_reads(self, starts, mtfs, slots=None):
         n = len(starts)
         s = np.ascontiguousarray(starts, dtype=np.int64)
         m = np.ascontiguousarray(mtfs, dtype=np.float64)
+        sl = np.ascontiguousarray(slots if slots is not None else np.arange(n), dtype=np.int32)
         info = (FieldInfo * n)()
-        self._check(self.lib.ldg_decode_reads(self.h, n, _ptr(s, C.c_int64), _ptr(m), info), 'ldg_decode_reads')
+        self._check(self.lib.ldg_decode_reads(self.h, n, _ptr(s, C.c_int64), _ptr(m), _ptr(sl, C.c_int32), info),
+                    'ldg_decode_reads')
         return list(info)
 
     def field_audio(self, slots, offsets):
