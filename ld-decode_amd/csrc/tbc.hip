@@ -7,9 +7,11 @@
 // (:1023-1035), downscale_audio (:431-484) and Framer.formatoutput (:1238-1252).
 //
 // Spline: scipy splrep(s=0) on unit-spaced points is the not-a-knot cubic
-// interpolant; it is solved exactly (no truncation) in second-derivative form
-// with a Thomas sweep, ONE LANE PER LINE: 64 lines per wave run their
-// recurrences side by side, and the Thomas scratch is lane-interleaved
+// interpolant; it is solved in second-derivative form with a Thomas sweep over
+// a window of rows reaching KTR=40 samples past the outputs a lane produces
+// (exact to rho^40 ~ 1e-23 relative, below double rounding).  The burst pass
+// runs one lane per line (40 outputs, ~100-row windows); the final pass splits
+// each line over 8 lanes.  The Thomas scratch is lane-interleaved
 // (dp[t*64 + lane]) so every step is a coalesced 512-byte access.
 #include <hip/hip_runtime.h>
 #include "common.hpp"
@@ -22,6 +24,8 @@ namespace {
 
 constexpr int SPL_MAXN = 2816;                 // max points per line (NTSC ~2545, PAL ~2563)
 constexpr int LINE_GROUPS = (MAX_LINES + 63) / 64;
+constexpr int FSEG = 8;                        // final pass: lanes per line
+constexpr int FGROUPS = MAX_LINES / (64 / FSEG); // final pass: workgroups per read
 
 struct CTab { double v[17]; };
 constexpr CTab make_ctab() {
@@ -33,57 +37,87 @@ constexpr CTab make_ctab() {
 __constant__ CTab g_ctab = make_ctab();        // Thomas c'_t for diag 4 / off-diag 1 (fixed point from t=14)
 __device__ __forceinline__ double ctab(int64_t t) { return g_ctab.v[t < 16 ? t : 16]; }
 
-// Not-a-knot cubic spline through y[j] = buf[ib + j], j = 0..n, evaluated at
-// x_o = o*step + x0 (numpy linspace(begin-ib, end-ib, W+1) arithmetic) for o in
-// [o_lo, o_hi), visiting o in descending order: sink(o, value).
-// dp: this lane's scratch, element t at dp[t * 64].  Returns 0, or -1 where
-// splrep would raise (too few / missing points).
-template <class Sink>
-__device__ int spline_eval(const double* __restrict__ buf, int64_t len, double begin, double end, int W, int o_lo,
-                           int o_hi, double* __restrict__ dp, Sink&& sink) {
+// Truncation margin of the windowed spline solve: the interior system
+// (1,4,1) couples M_j to its neighbours with decay rho = 2 - sqrt(3) per
+// sample, so cutting the system KTR rows beyond the needed range perturbs
+// the result by < rho^KTR ~ 1.5e-23 (relative) -- below double rounding.
+constexpr int KTR = 40;
+constexpr int SCR_LANE = 512;                 // Thomas scratch entries per lane
+constexpr int64_t SCR_PER_SLOT = (int64_t)FGROUPS * 64 * SCR_LANE;
+
+// Not-a-knot cubic spline through y[j] = buf[ib + j], j = 0..n (lddutils.scale:
+// splrep(s=0) on unit spacing), evaluated at x_o = o*step + x0 (numpy
+// linspace(begin-ib, end-ib, W+1) arithmetic) for o in [o_lo, o_hi), visiting o
+// in descending order: sink(o, value).
+//
+// Second-derivative form.  The not-a-knot rows fold into M_1 = r_1/6 and
+// M_{n-1} = r_{n-1}/6; rows 2..n-2 are tridiagonal (1,4,1).  Only the rows
+// [jlo-KTR, jhi+1+KTR] around the intervals the requested outputs fall in are
+// solved (exact boundary values where the window reaches a line end), so a
+// line can be split over several lanes.  dp: this lane's scratch, entry t at
+// dp[t * ST].  Returns 0, or -1 where splrep would raise.
+template <int ST, class Sink>
+__device__ int spline_window(const double* __restrict__ buf, int64_t len, double begin, double end, int W, int o_lo,
+                             int o_hi, double* __restrict__ dp, Sink&& sink) {
   const int64_t ib = py_int(begin), ie = py_int(end);
   const int64_t n = ie - ib;
   if (ib < 0 || n < 6 || n >= SPL_MAXN || ib + n + 1 > len) return -1;
   const double* y = buf + ib;
   auto rr = [&](int64_t j) { return 6.0 * ((y[j + 1] - y[j]) - (y[j] - y[j - 1])); };
-  const double M1 = rr(1) / 6.0, Mn1 = rr(n - 1) / 6.0;   // not-a-knot rows folded in
-  const int64_t N = n - 3;                                 // unknowns M_2 .. M_{n-2}
-  double dprev = 0.0;
-  for (int64_t t = 0; t < N; t++) {
-    double rhs = rr(t + 2);
-    if (t == 0) rhs -= M1;
-    if (t == N - 1) rhs -= Mn1;
-    const double d = (rhs - dprev) * ctab(t);
-    dp[t * 64] = d;
-    dprev = d;
-  }
+  const double M1 = rr(1) / 6.0, Mn1 = rr(n - 1) / 6.0;
   const double x0 = begin - (double)ib;
   const double span = end - begin;
   const double step = ((span + x0) - x0) / (double)W;
-  const double Mn2 = dp[(N - 1) * 64];
-  double Mk1 = 2.0 * Mn1 - Mn2;   // M_n
-  double M2 = 0.0;
+  auto xo = [&](int o) { double x = (double)o * step; return x + x0; };
+  auto ival = [&](double x) {
+    int64_t j = (int64_t)floor(x);
+    return j < 0 ? (int64_t)0 : (j > n - 1 ? n - 1 : j);
+  };
+  const int64_t jlo = ival(xo(o_lo)), jhi = ival(xo(o_hi - 1));
+  const int64_t lo = (jlo - KTR > 2) ? jlo - KTR : 2;
+  const int64_t hi = (jhi + 1 + KTR < n - 2) ? jhi + 1 + KTR : n - 2;
+  const int64_t N = hi - lo + 1;
+  if (N > SCR_LANE) return -1;
+  const double BL = (lo == 2) ? M1 : 0.0, BR = (hi == n - 2) ? Mn1 : 0.0;
+  double dprev = 0.0;
+  for (int64_t t = 0; t < N; t++) {
+    double rhs = rr(lo + t);
+    if (t == 0) rhs -= BL;
+    if (t == N - 1) rhs -= BR;
+    const double d = (rhs - dprev) * ctab(t);
+    dp[t * ST] = d;
+    dprev = d;
+  }
   int o = o_hi - 1;
-  for (int64_t k = n - 1; k >= 0 && o >= o_lo; k--) {
-    double Mk;
-    if (k == n - 1) Mk = Mn1;
-    else if (k >= 2) {
-      const int64_t t = k - 2;
-      Mk = (t == N - 1) ? dp[t * 64] : dp[t * 64] - ctab(t) * Mk1;
-    } else if (k == 1) Mk = M1;
-    else Mk = 2.0 * M1 - M2;
-    if (k == 2) M2 = Mk;
+  auto emit = [&](int64_t k, double Mk, double Mk1, bool lowest) {
     const double yk = y[k], yk1 = y[k + 1];
     while (o >= o_lo) {
-      double x = (double)o * step;
-      x = x + x0;
-      if (k > 0 && x < (double)k) break;
+      const double x = xo(o);
+      if (!lowest && x < (double)k) break;
       const double a = (double)(k + 1) - x, b = x - (double)k;
       const double v = Mk * a * a * a / 6.0 + Mk1 * b * b * b / 6.0 + (yk - Mk / 6.0) * a + (yk1 - Mk1 / 6.0) * b;
       sink(o, v);
       o--;
     }
-    Mk1 = Mk;
+  };
+  const double Mhi = dp[(N - 1) * ST];
+  double Mnext = 0.0;                        // M_{k+1}
+  if (hi == n - 2) {
+    // interval n-1: (M_{n-1}, M_n = 2 M_{n-1} - M_{n-2}) -- the not-a-knot end piece
+    if (jhi == n - 1) emit(n - 1, Mn1, 2.0 * Mn1 - Mhi, jlo == n - 1);
+    Mnext = Mn1;
+  }
+  const int64_t kstop = jlo > lo ? jlo : lo;
+  for (int64_t k = hi; k >= kstop && o >= o_lo; k--) {
+    const int64_t t = k - lo;
+    const double Mk = (t == N - 1) ? Mhi : dp[t * ST] - ctab(t) * Mnext;
+    if (k <= jhi) emit(k, Mk, Mnext, k == jlo);
+    Mnext = Mk;
+  }
+  if (o >= o_lo && jlo < lo) {               // lo == 2: the not-a-knot start piece
+    const double M2 = Mnext;
+    if (jhi >= 1) emit(1, M1, M2, jlo == 1);
+    if (o >= o_lo) emit(0, 2.0 * M1 - M2, M1, true);
   }
   return 0;
 }
@@ -149,13 +183,14 @@ extern "C" __global__ __launch_bounds__(64) void ldg_k_burst_lines(
   if (l >= nl) return;
   if (l >= lc) { pv0[l] = 0.0; pv1[l] = 0.0; lvl[l] = 0.0f; return; }
   const double* bur = video + (int64_t)slot * vread_stride + (int64_t)CH_BURST * vchan_stride;
-  double* dp = scratch + (((int64_t)slot * LINE_GROUPS + grp) * SPL_MAXN) * 64 + lane;
+  double* dp = scratch + (int64_t)slot * SCR_PER_SLOT + (int64_t)grp * 64 * SCR_LANE + lane;
   double* ba = s_ba + lane;
   double* tt = s_t + lane;
   const double b0 = li[l], b1 = li[l + 1];
   const double wow = (b1 - b0) / (double)C.linelen;
   const int W = C.outlinelen;
-  const int rc = spline_eval(bur, R->n_out, b0, b1, W, 20, 60, dp, [&](int o, double v) { ba[(o - 20) * 64] = v * wow; });
+  const int rc = spline_window<64>(bur, R->n_out, b0, b1, W, 20, 60, dp,
+                                   [&](int o, double v) { ba[(o - 20) * 64] = v * wow; });
   if (rc < 0) { R->status = FS_TBC; return; }   // benign race: every writer stores the same value
 
   const double hzs = 1700000 / 140.0;
@@ -280,22 +315,23 @@ extern "C" __global__ __launch_bounds__(64) void ldg_k_burst_field(const int32_t
 // lines (lddecode_core.py:1135-1159 NTSC, :1023-1035 PAL).
 // grid: n_reads * LINE_GROUPS workgroups of 64 threads; lane = output row.
 extern "C" __global__ __launch_bounds__(64) void ldg_k_final_lines(
-    const int32_t* __restrict__ smap, const double* __restrict__ video, int64_t vread_stride, int64_t vchan_stride, SysConst C,
-    FieldRec* __restrict__ recs, const double* __restrict__ lines, const float* __restrict__ blevel,
+    const int32_t* __restrict__ smap, const double* __restrict__ video, int64_t vread_stride, int64_t vchan_stride,
+    SysConst C, FieldRec* __restrict__ recs, const double* __restrict__ lines, const float* __restrict__ blevel,
     double* __restrict__ scratch, uint16_t* __restrict__ pic, int64_t pic_stride) {
   const int lane = threadIdx.x;
-  const int slot = smap[blockIdx.x / LINE_GROUPS];
-  const int grp = blockIdx.x % LINE_GROUPS;
+  const int slot = smap[blockIdx.x / FGROUPS];
+  const int grp = blockIdx.x % FGROUPS;
   FieldRec* R = recs + slot;
   if (R->status != FS_PENDING) return;
-  const int row = grp * 64 + lane;
+  const int row = grp * (64 / FSEG) + lane / FSEG;   // FSEG lanes share one output line
+  const int seg = lane % FSEG;
   const int lc = R->linecount;
   if (row >= lc) return;
   const int loff = (C.system == 1) ? 3 : 1;
   const int l = row + loff;
   const double* lf = lines + (int64_t)slot * LINES_STRIDE + LLF * MAX_LINES;
   const double* dm = video + (int64_t)slot * vread_stride + (int64_t)CH_DEMOD * vchan_stride;
-  double* dp = scratch + (((int64_t)slot * LINE_GROUPS + grp) * SPL_MAXN) * 64 + lane;
+  double* dp = scratch + (int64_t)slot * SCR_PER_SLOT + (int64_t)grp * 64 * SCR_LANE + lane;
   const int W = C.outlinelen;
   uint16_t* out = pic + (int64_t)slot * pic_stride + (int64_t)row * W;
   const double b0 = lf[l], b1 = lf[l + 1];
@@ -304,7 +340,8 @@ extern "C" __global__ __launch_bounds__(64) void ldg_k_final_lines(
   const double scale_ = pal ? (double)(0xd300 - 0x0100) / (100 - C.vsync_ire)
                             : (double)(0xc800 - 0x0400) / (100 - C.vsync_ire);
   const double base = pal ? 256.0 : 1024.0;
-  const int rc = spline_eval(dm, R->n_out, b0, b1, W, 0, W, dp, [&](int o, double v) {
+  const int o_lo = seg * W / FSEG, o_hi = (seg + 1) * W / FSEG;
+  const int rc = spline_window<64>(dm, R->n_out, b0, b1, W, o_lo, o_hi, dp, [&](int o, double v) {
     double red = ((v * wow) - C.ire0) / C.hz_ire;
     red -= C.vsync_ire;
     double x = (red * scale_) + base;
@@ -313,7 +350,7 @@ extern "C" __global__ __launch_bounds__(64) void ldg_k_final_lines(
     out[o] = (uint16_t)x;
   });
   if (rc < 0) { R->status = FS_TBC; return; }
-  if (!pal && row >= 1 && row < lc - 1) {
+  if (!pal && seg == 0 && row >= 1 && row < lc - 1) {
     const float bl = blevel[(int64_t)slot * MAX_LINES + row];
     const double hzs = 1700000 / 140.0;
     out[0] = bl > 0 ? 16384 : 32768;
@@ -407,7 +444,7 @@ extern "C" __global__ __launch_bounds__(256) void ldg_k_frames(const int32_t* __
 namespace {
 constexpr int PILOT_MAX = 64;
 __device__ __forceinline__ double* pilot_base(double* scratch, int slot) {
-  return scratch + (int64_t)slot * LINE_GROUPS * SPL_MAXN * 64;
+  return scratch + (int64_t)slot * SCR_PER_SLOT;
 }
 }  // namespace
 
