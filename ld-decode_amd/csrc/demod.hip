@@ -23,7 +23,6 @@ namespace {
 
 constexpr int T = 1024;
 constexpr int M = HALF;           // 8192
-constexpr int LDSN = M + M / 8;   // padded
 
 __device__ __forceinline__ double load_sample(const uint8_t* __restrict__ cap, int fmt, int64_t rel) {
   if (fmt == 0) return (double)cap[rel];
@@ -71,48 +70,68 @@ __device__ __forceinline__ double fold_tau(double d) {
   return d < 0.0 ? d + TAU : d;
 }
 
+// Half-spectrum bins k in [0, M/2] paired with M-k: thread tid owns
+// k = tid + 1024 q (q < 4) and, thread 0 only, k = M/2 (slot 4).
 struct Pairs {
   double2 a[5], b[5];   // value at k and at M-k of each pair slot
 };
+
+// Opaque copy of tid: stops the compiler from hoisting per-lane twiddle loads
+// and addresses that repeat across the kernel's transforms (and spilling them).
+__device__ __forceinline__ int fresh(int tid) { asm volatile("" : "+v"(tid)); return tid; }
 
 __device__ __forceinline__ int pair_k(int tid, int q) { return q < 4 ? tid + 1024 * q : 4096; }
 __device__ __forceinline__ bool pair_live(int tid, int q) { return q < 4 || tid == 0; }
 
 // Half-spectrum of the real signal currently transformed in LDS, for my pairs.
-__device__ __forceinline__ void split_pairs(const double* re, const double* im, const double2* __restrict__ tw,
-                                            int tid, Pairs& X) {
+__device__ __forceinline__ void split_pairs(CBuf x, const double2* __restrict__ tw, int tid, Pairs& X) {
+  tid = fresh(tid);
 #pragma unroll
   for (int q = 0; q < 5; q++) {
     if (!pair_live(tid, q)) continue;
     const int k = pair_k(tid, q), kp = M - k;
-    const double2 A = make_double2(re[PAD(k)], im[PAD(k)]);
-    const double2 B = make_double2(re[PAD(kp & (M - 1))], im[PAD(kp & (M - 1))]);
+    const double2 A = x[k];
+    const double2 B = x[kp & (M - 1)];
     X.a[q] = rsplit(A, B, tw[k]);
     X.b[q] = rsplit(B, A, tw[kp]);
   }
 }
 
-// Write merge(D * G) for my pairs into LDS (input of a C2R inverse FFT).
-__device__ __forceinline__ void merge_filtered(double* re, double* im, const double2* __restrict__ tw,
-                                               const double2* __restrict__ G, int tid, const Pairs& D) {
+// Split the real-signal spectrum in LDS and park my pairs in global memory
+// (slot 2q: bin k, slot 2q+1: bin M-k; coalesced, this lane's own entries).
+__device__ __forceinline__ void park_split(CBuf x, const double2* __restrict__ tw, int tid, double2* __restrict__ park) {
+  tid = fresh(tid);
 #pragma unroll
   for (int q = 0; q < 5; q++) {
     if (!pair_live(tid, q)) continue;
     const int k = pair_k(tid, q), kp = M - k;
-    const double2 Pk = cmul(D.a[q], G[k]);
-    const double2 Pkp = cmul(D.b[q], G[kp]);
-    const double2 zk = cmerge(Pk, Pkp, tw[k]);
-    re[PAD(k)] = zk.x; im[PAD(k)] = zk.y;
-    if (kp < M && kp != k) {
-      const double2 zkp = cmerge(Pkp, Pk, tw[kp]);
-      re[PAD(kp)] = zkp.x; im[PAD(kp)] = zkp.y;
-    }
+    const double2 A = x[k];
+    const double2 B = x[kp & (M - 1)];
+    park[(2 * q) * T] = rsplit(A, B, tw[k]);
+    park[(2 * q + 1) * T] = rsplit(B, A, tw[kp]);
+  }
+}
+
+// Write merge(D * G) for my parked pairs into LDS (input of a C2R inverse FFT).
+__device__ __forceinline__ void merge_filtered(CBuf x, const double2* __restrict__ tw, const double2* __restrict__ G,
+                                               int tid, const double2* __restrict__ park) {
+  tid = fresh(tid);
+#pragma unroll
+  for (int q = 0; q < 5; q++) {
+    if (!pair_live(tid, q)) continue;
+    const int k = pair_k(tid, q), kp = M - k;
+    const double2 Pk = cmul(park[(2 * q) * T], G[k]);
+    const double2 Pkp = cmul(park[(2 * q + 1) * T], G[kp]);
+    x[k] = cmerge(Pk, Pkp, tw[k]);
+    if (kp < M && kp != k) x[kp] = cmerge(Pkp, Pk, tw[kp]);
   }
 }
 
 }  // namespace
 
 // grid: n_reads * MAX_BLOCKS_PER_READ workgroups of 1024 threads.
+// ospill: 10 x 1024 double2 per workgroup (the odd-half analytic spectrum is
+// parked there, coalesced, while the even half is transformed).
 extern "C" __global__ __launch_bounds__(1024) void ldg_k_demod(
     const int32_t* __restrict__ smap, const ReadDesc* __restrict__ reads, const uint8_t* __restrict__ cap, int64_t cap_first, int64_t cap_nsamp,
     int fmt, const double2* __restrict__ tw, const double2* __restrict__ rf_filt,
@@ -120,9 +139,11 @@ extern "C" __global__ __launch_bounds__(1024) void ldg_k_demod(
     const double2* __restrict__ g_pilot, const double2* __restrict__ g_psync,
     const double2* __restrict__ a_lfilt, const double2* __restrict__ a_rfilt, SysConst C,
     double* __restrict__ video, int64_t vread_stride, int64_t vchan_stride,
-    double* __restrict__ audio1, int64_t aread_stride, int64_t achan_stride, int32_t* __restrict__ status) {
-  __shared__ double s_re[LDSN];
-  __shared__ double s_im[LDSN];
+    double* __restrict__ audio1, int64_t aread_stride, int64_t achan_stride, int32_t* __restrict__ status,
+    double2* __restrict__ ospill) {
+  __shared__ double2 s_x[M];          // 128 KiB: the 8192-point transforms
+  __shared__ double2 s_a[2048];       // 32 KiB: the two 1024-point audio transforms
+  const CBuf X_{s_x}, A_{s_a};
   const int tid = threadIdx.x;
   const int slot = smap[blockIdx.x / MAX_BLOCKS_PER_READ];
   const int b = blockIdx.x % MAX_BLOCKS_PER_READ;
@@ -139,62 +160,77 @@ extern "C" __global__ __launch_bounds__(1024) void ldg_k_demod(
   }
   double* vout = video + (int64_t)slot * vread_stride + off - BLOCKCUT;   // index by block position p
   const double2* F = rf_filt + (int64_t)rd.filt_slot * BLOCKLEN;
+  double2* osp = ospill + (int64_t)blockIdx.x * 10 * T + tid;
   constexpr double TAU = 6.283185307179586;
 
   // ---- 1. raw samples -> z[m] = x[2m] + i x[2m+1]; forward FFT ---------------
 #pragma unroll
   for (int q = 0; q < 8; q++) {
     const int m = tid + T * q;
-    s_re[PAD(m)] = load_sample(cap, fmt, rel0 + 2 * m);
-    s_im[PAD(m)] = load_sample(cap, fmt, rel0 + 2 * m + 1);
+    X_[m] = make_double2(load_sample(cap, fmt, rel0 + 2 * m), load_sample(cap, fmt, rel0 + 2 * m + 1));
   }
-  fft_lds<M, T, false>(s_re, s_im, tw, tid);
+  fft_lds<M, T, false>(X_, tw, tid);
 
-  Pairs X;
-  split_pairs(s_re, s_im, tw, tid, X);
-  __syncthreads();
-
-  // ---- 2. audio phase 1: carrier slices -> 2 x IFFT1024 -> FM demod ------------
-  // lddecode_core.py:321-328; slices audio_fdslice (lo [a0,a0+512), hi mirrored).
+  // ---- 2. analytic-signal spectra and the audio carrier slices ---------------
+  // Y = X * RFVideo*MTF^m; the 16384-point IFFT of Y is done as its even/odd
+  // (radix-2 DIF) halves: even half -> LDS, odd half -> ospill.  The audio
+  // slices (lddecode_core.py:321-328, audio_fdslice lo [a0,a0+512), hi
+  // mirrored) go to the separate 32 KiB audio buffer.  X dies here.
   {
+    Pairs X;
+    split_pairs(X_, tw, tid, X);
+    __syncthreads();
     const int a0 = C.audio_lo0;
-    double* LR = s_re;            // left at [0,1024), right at [1024,2048) (padded)
-    double* LI = s_im;
 #pragma unroll
-    for (int q = 0; q < 4; q++) {
-      const int k = pair_k(tid, q);
-      const double2 xk = X.a[q];
-      if (k >= a0 && k < a0 + 512) {
-        const int j = k - a0;
-        const double2 l = cmul(xk, a_lfilt[j]), r = cmul(xk, a_rfilt[j]);
-        LR[PAD(j)] = l.x; LI[PAD(j)] = l.y;
-        LR[PAD(1024 + j)] = r.x; LI[PAD(1024 + j)] = r.y;
+    for (int q = 0; q < 5; q++) {
+      if (!pair_live(tid, q)) continue;
+      const int k = pair_k(tid, q), kp = M - k;
+      if (q < 4) {
+        const double2 xk = X.a[q];
+        if (k >= a0 && k < a0 + 512) {
+          const int j = k - a0;
+          A_[j] = cmul(xk, a_lfilt[j]);            // left at [0,1024), right at [1024,2048)
+          A_[1024 + j] = cmul(xk, a_rfilt[j]);
+        }
+        if (k > a0 && k <= a0 + 512) {
+          const int j = a0 + 1024 - k;
+          const double2 xc = conj2(xk);
+          A_[j] = cmul(xc, a_lfilt[j]);
+          A_[1024 + j] = cmul(xc, a_rfilt[j]);
+        }
       }
-      if (k > a0 && k <= a0 + 512) {
-        const int j = a0 + 1024 - k;
-        const double2 xc = conj2(xk);
-        const double2 l = cmul(xc, a_lfilt[j]), r = cmul(xc, a_rfilt[j]);
-        LR[PAD(j)] = l.x; LI[PAD(j)] = l.y;
-        LR[PAD(1024 + j)] = r.x; LI[PAD(1024 + j)] = r.y;
+      const double2 yk = cmul(X.a[q], F[k]);
+      const double2 yk2 = cmul(conj2(X.b[q]), F[k + M]);
+      X_[k] = cadd(yk, yk2);
+      osp[(2 * q) * T] = cmulc(csub(yk, yk2), tw[k]);
+      if (kp < M && kp != k) {
+        const double2 ykp = cmul(X.b[q], F[kp]);
+        const double2 ykp2 = cmul(conj2(X.a[q]), F[kp + M]);
+        X_[kp] = cadd(ykp, ykp2);
+        osp[(2 * q + 1) * T] = cmulc(csub(ykp, ykp2), tw[kp]);
       }
     }
+  }
+
+  // ---- 3. audio phase 1: 2 x IFFT1024 -> FM demod (lddecode_core.py:321-328) ----
+  {
     const int g = tid >> 9, lt = tid & 511;
-    double* gre = s_re + (g ? PAD(1024) : 0);
-    double* gim = s_im + (g ? PAD(1024) : 0);
-    fft_lds<1024, 512, true>(gre, gim, tw, lt);
+    const CBuf ga = A_ + (g ? 1024 : 0);
+    fft_lds<1024, 512, true>(ga, tw, lt);
     double th[2];
 #pragma unroll
-    for (int e = 0; e < 2; e++) { const int p = lt + 512 * e; th[e] = atan2(gim[PAD(p)], gre[PAD(p)]); }
+    for (int e = 0; e < 2; e++) { const double2 z = ga[lt + 512 * e]; th[e] = atan2(z.y, z.x); }
     __syncthreads();
+    double* gth = reinterpret_cast<double*>(s_a) + (g ? 1024 : 0);     // plain (unswizzled) phase scratch
 #pragma unroll
-    for (int e = 0; e < 2; e++) gre[PAD(lt + 512 * e)] = th[e];
+    for (int e = 0; e < 2; e++) gth[lt + 512 * e] = th[e];
     __syncthreads();
     double* aout = audio1 + (int64_t)slot * aread_stride + (int64_t)g * achan_stride;
     const int kept = copylen / AUDIO_DIV1;
 #pragma unroll
     for (int e = 0; e < 2; e++) {
       const int p = lt + 512 * e;
-      const double prev = p ? gre[PAD(p - 1)] : 0.0;
+      const double prev = p ? gth[p - 1] : 0.0;
       const double d = p ? fold_tau(th[e] - prev) : 0.0;
       const double v = d * (C.freq_arf / TAU) + C.audio_lowfreq;
       const int j = p - BLOCKCUT / AUDIO_DIV1;
@@ -205,79 +241,62 @@ extern "C" __global__ __launch_bounds__(1024) void ldg_k_demod(
       const int last = (off + copylen) / AUDIO_DIV1;
       for (int j = last + lt; j < rd.n_audio; j += 512) aout[j] = 0.0;
     }
-    __syncthreads();
   }
 
-  // ---- 3. analytic signal: Y = X * RFVideo*MTF^m; IFFT16384 via even/odd halves --
-  Pairs O;
-#pragma unroll
-  for (int q = 0; q < 5; q++) {
-    if (!pair_live(tid, q)) continue;
-    const int k = pair_k(tid, q), kp = M - k;
-    const double2 yk = cmul(X.a[q], F[k]);
-    const double2 yk2 = cmul(conj2(X.b[q]), F[k + M]);
-    const double2 ek = cadd(yk, yk2);
-    O.a[q] = cmulc(csub(yk, yk2), tw[k]);
-    s_re[PAD(k)] = ek.x; s_im[PAD(k)] = ek.y;
-    if (kp < M && kp != k) {
-      const double2 ykp = cmul(X.b[q], F[kp]);
-      const double2 ykp2 = cmul(conj2(X.a[q]), F[kp + M]);
-      const double2 ekp = cadd(ykp, ykp2);
-      O.b[q] = cmulc(csub(ykp, ykp2), tw[kp]);
-      s_re[PAD(kp)] = ekp.x; s_im[PAD(kp)] = ekp.y;
-    }
-  }
-  fft_lds<M, T, true>(s_re, s_im, tw, tid);
+  // ---- 4. analytic IFFTs (even, odd) -> instantaneous phase --------------------
+  fft_lds<M, T, true>(X_, tw, tid);
   double the[8], tho[8];
 #pragma unroll
-  for (int q = 0; q < 8; q++) { const int m = tid + T * q; the[q] = atan2(s_im[PAD(m)], s_re[PAD(m)]); }
+  for (int q = 0; q < 8; q++) { const double2 z = X_[tid + T * q]; the[q] = atan2(z.y, z.x); }
   __syncthreads();
 #pragma unroll
   for (int q = 0; q < 5; q++) {
     if (!pair_live(tid, q)) continue;
     const int k = pair_k(tid, q), kp = M - k;
-    s_re[PAD(k)] = O.a[q].x; s_im[PAD(k)] = O.a[q].y;
-    if (kp < M && kp != k) { s_re[PAD(kp)] = O.b[q].x; s_im[PAD(kp)] = O.b[q].y; }
+    X_[k] = osp[(2 * q) * T];
+    if (kp < M && kp != k) X_[kp] = osp[(2 * q + 1) * T];
   }
-  fft_lds<M, T, true>(s_re, s_im, tw, tid);
+  fft_lds<M, T, true>(X_, tw, tid);
 #pragma unroll
-  for (int q = 0; q < 8; q++) { const int m = tid + T * q; tho[q] = atan2(s_im[PAD(m)], s_re[PAD(m)]); }
+  for (int q = 0; q < 8; q++) { const double2 z = X_[tid + T * q]; tho[q] = atan2(z.y, z.x); }
   __syncthreads();
+  double* ph = reinterpret_cast<double*>(s_x);    // plain (unswizzled) phase scratch
 #pragma unroll
-  for (int q = 0; q < 8; q++) s_re[PAD(tid + T * q)] = tho[q];
+  for (int q = 0; q < 8; q++) ph[tid + T * q] = tho[q];
   __syncthreads();
 
-  // ---- 4. FM demod (Hz) -> demod spectrum D ----------------------------------
+  // ---- 5. FM demod (Hz) -> demod spectrum D (parked in ospill) ----------------------------------
   {
     const double hzk = C.freq_hz / TAU;
     double d0[8], d1[8];
 #pragma unroll
     for (int q = 0; q < 8; q++) {
       const int m = tid + T * q;
-      const double prev = m ? s_re[PAD(m - 1)] : 0.0;
+      const double prev = m ? ph[m - 1] : 0.0;
       d0[q] = m ? fold_tau(the[q] - prev) * hzk : 0.0;
       d1[q] = fold_tau(tho[q] - the[q]) * hzk;
     }
     __syncthreads();
 #pragma unroll
-    for (int q = 0; q < 8; q++) { const int m = tid + T * q; s_re[PAD(m)] = d0[q]; s_im[PAD(m)] = d1[q]; }
+    for (int q = 0; q < 8; q++) X_[tid + T * q] = make_double2(d0[q], d1[q]);
   }
-  fft_lds<M, T, false>(s_re, s_im, tw, tid);
-  Pairs D;
-  split_pairs(s_re, s_im, tw, tid, D);
+  fft_lds<M, T, false>(X_, tw, tid);
+  park_split(X_, tw, tid, osp);
   __syncthreads();
 
   const double inv = 1.0 / (double)M;
   auto emit = [&](int ch, const double2* G) {
-    merge_filtered(s_re, s_im, tw, G, tid, D);
-    fft_lds<M, T, true>(s_re, s_im, tw, tid);
+    merge_filtered(X_, tw, G, tid, osp);
+    fft_lds<M, T, true>(X_, tw, tid);
     double* o = vout + (int64_t)ch * vchan_stride;
+    const int t = fresh(tid);
 #pragma unroll
     for (int q = 0; q < 8; q++) {
-      const int m = tid + T * q;
+      const int m = t + T * q;
       const int p = 2 * m;
-      if (p >= BLOCKCUT && p < BLOCKCUT + copylen) o[p] = s_re[PAD(m)] * inv;
-      if (p + 1 >= BLOCKCUT && p + 1 < BLOCKCUT + copylen) o[p + 1] = s_im[PAD(m)] * inv;
+      const double2 z = X_[m];
+      if (p >= BLOCKCUT && p < BLOCKCUT + copylen) o[p] = z.x * inv;
+      if (p + 1 >= BLOCKCUT && p + 1 < BLOCKCUT + copylen) o[p + 1] = z.y * inv;
     }
     __syncthreads();
   };
@@ -285,18 +304,19 @@ extern "C" __global__ __launch_bounds__(1024) void ldg_k_demod(
   emit(CH_BURST, g_burst);
   if (C.n_chan > 4) emit(CH_PILOT, g_pilot);
 
-  // ---- 5. 0.5 MHz channel (rolled by -F05_offset) and the sync detector --------
-  merge_filtered(s_re, s_im, tw, g_05, tid, D);
-  fft_lds<M, T, true>(s_re, s_im, tw, tid);
+  // ---- 6. 0.5 MHz channel (rolled by -F05_offset) and the sync detector --------
+  merge_filtered(X_, tw, g_05, tid, osp);
+  fft_lds<M, T, true>(X_, tw, tid);
   {
     double v0[8], v1[8];
 #pragma unroll
-    for (int q = 0; q < 8; q++) { const int m = tid + T * q; v0[q] = s_re[PAD(m)] * inv; v1[q] = s_im[PAD(m)] * inv; }
+    for (int q = 0; q < 8; q++) { const double2 z = X_[tid + T * q]; v0[q] = z.x * inv; v1[q] = z.y * inv; }
     __syncthreads();
     double* o = vout + (int64_t)CH_05 * vchan_stride;
+    const int t = fresh(tid);
 #pragma unroll
     for (int q = 0; q < 8; q++) {
-      const int m = tid + T * q;
+      const int m = t + T * q;
       // value at block position p lands at rolled position (p - 32) mod 16384
       const int p0 = (2 * m - BLOCKCUT_END) & (BLOCKLEN - 1);
       const int p1 = (2 * m + 1 - BLOCKCUT_END) & (BLOCKLEN - 1);
@@ -304,12 +324,12 @@ extern "C" __global__ __launch_bounds__(1024) void ldg_k_demod(
       if (p1 >= BLOCKCUT && p1 < BLOCKCUT + copylen) o[p1] = v1[q];
       // inrange(demod_05, iretohz(-55), iretohz(-25)) as 0/1 doubles
       const int mz = (m - BLOCKCUT_END / 2) & (M - 1);
-      s_re[PAD(mz)] = (v0[q] >= C.sync_lo && v0[q] <= C.sync_hi) ? 1.0 : 0.0;
-      s_im[PAD(mz)] = (v1[q] >= C.sync_lo && v1[q] <= C.sync_hi) ? 1.0 : 0.0;
+      X_[mz] = make_double2((v0[q] >= C.sync_lo && v0[q] <= C.sync_hi) ? 1.0 : 0.0,
+                            (v1[q] >= C.sync_lo && v1[q] <= C.sync_hi) ? 1.0 : 0.0);
     }
   }
-  fft_lds<M, T, false>(s_re, s_im, tw, tid);
-  split_pairs(s_re, s_im, tw, tid, D);
+  fft_lds<M, T, false>(X_, tw, tid);
+  park_split(X_, tw, tid, osp);
   __syncthreads();
   emit(CH_SYNC, g_psync);
 }
@@ -323,8 +343,8 @@ extern "C" __global__ __launch_bounds__(1024) void ldg_k_audio2(
     const int32_t* __restrict__ smap, const ReadDesc* __restrict__ reads, const double2* __restrict__ tw, const double2* __restrict__ lpf2,
     const double* __restrict__ audio1, int64_t aread_stride, int64_t achan_stride,
     double* __restrict__ audio2, int64_t a2read_stride, int64_t a2chan_stride, const int32_t* __restrict__ status) {
-  __shared__ double s_re[LDSN];
-  __shared__ double s_im[LDSN];
+  __shared__ double2 s_x[M];
+  const CBuf X_{s_x};
   const int tid = threadIdx.x;
   const int ch = blockIdx.x & 1;
   const int j = (blockIdx.x >> 1) & 7;
@@ -342,21 +362,16 @@ extern "C" __global__ __launch_bounds__(1024) void ldg_k_audio2(
 #pragma unroll
   for (int q = 0; q < 8; q++) {
     const int m = tid + T * q;
-    s_re[PAD(m)] = src[2 * m];
-    s_im[PAD(m)] = src[2 * m + 1];
+    X_[m] = make_double2(src[2 * m], src[2 * m + 1]);
   }
-  fft_lds<M, T, false>(s_re, s_im, tw, tid);
+  fft_lds<M, T, false>(X_, tw, tid);
   // X[k] for k in [0, 2048]
   double2 xa, xb, xc = make_double2(0, 0);
   {
     const int k1 = tid, k2 = tid + 1024;
-    xa = rsplit(make_double2(s_re[PAD(k1)], s_im[PAD(k1)]),
-                make_double2(s_re[PAD((M - k1) & (M - 1))], s_im[PAD((M - k1) & (M - 1))]), tw[k1]);
-    xb = rsplit(make_double2(s_re[PAD(k2)], s_im[PAD(k2)]),
-                make_double2(s_re[PAD(M - k2)], s_im[PAD(M - k2)]), tw[k2]);
-    if (tid == 0)
-      xc = rsplit(make_double2(s_re[PAD(2048)], s_im[PAD(2048)]),
-                  make_double2(s_re[PAD(M - 2048)], s_im[PAD(M - 2048)]), tw[2048]);
+    xa = rsplit(X_[k1], X_[(M - k1) & (M - 1)], tw[k1]);
+    xb = rsplit(X_[k2], X_[M - k2], tw[k2]);
+    if (tid == 0) xc = rsplit(X_[2048], X_[M - 2048], tw[2048]);
   }
   __syncthreads();
   // S[j] = X[j] (j < 2048); S[j] = conj(X[4096 - j]) (j >= 2048); times lpf2
@@ -366,27 +381,22 @@ extern "C" __global__ __launch_bounds__(1024) void ldg_k_audio2(
 #pragma unroll
     for (int e = 0; e < 2; e++) {
       const int k = ks[e];
-      const double2 s = cmul(xs[e], lpf2[k]);
-      s_re[PAD(k)] = s.x; s_im[PAD(k)] = s.y;
+      X_[k] = cmul(xs[e], lpf2[k]);
       if (k >= 1) {
         const int jj = AUDIO2_BLOCK - k;
-        const double2 t = cmul(conj2(xs[e]), lpf2[jj]);
-        s_re[PAD(jj)] = t.x; s_im[PAD(jj)] = t.y;
+        X_[jj] = cmul(conj2(xs[e]), lpf2[jj]);
       }
     }
-    if (tid == 0) {
-      const double2 t = cmul(conj2(xc), lpf2[2048]);
-      s_re[PAD(2048)] = t.x; s_im[PAD(2048)] = t.y;
-    }
+    if (tid == 0) X_[2048] = cmul(conj2(xc), lpf2[2048]);
   }
-  fft_lds<AUDIO2_BLOCK, 512, true>(s_re, s_im, tw, tid);   // threads >= 512 only join barriers
+  fft_lds<AUDIO2_BLOCK, 512, true>(X_, tw, tid);   // threads >= 512 only join barriers
   double* dst = audio2 + (int64_t)slot * a2read_stride + (int64_t)ch * a2chan_stride;
   const double scale = 1.0 / (double)AUDIO2_BLOCK / (double)AUDIO_DIV2;
   const int last_start = n_out - (AUDIO2_BLOCK - SKIP);
 #pragma unroll
   for (int e = 0; e < 4; e++) {
     const int p = tid + 1024 * e;
-    const double v = s_re[PAD(p)] * scale;
+    const double v = X_[p].x * scale;
     int o;
     if (j == 0) {
       o = p;

@@ -1,15 +1,19 @@
 // Workgroup-level FP64 FFT for gfx950, LDS-resident, Stockham autosort.
 //
-// Data lives in two LDS arrays (re / im, structure-of-arrays) indexed through
-// PAD(i) = i + i/8: one pad double every 8 keeps the stride-R writes of the
-// early Stockham passes conflict-free for ds_write_b64 (bank = dword mod 32)
-// while the unit-stride reads stay conflict-free.  An 8192-point complex FFT
-// therefore needs 2 * 9216 * 8 B = 144 KiB of the 160 KiB LDS.
+// Data lives in LDS as interleaved complex doubles (one 16-byte double2 per
+// point, ds_read_b128 / ds_write_b128) under an XOR swizzle
+//     slot(i) = i ^ ((i >> 3) & 7)
+// that permutes points inside aligned groups of 8.  Unit-stride reads stay a
+// permutation of 16 consecutive slots (64 banks, conflict-free for the
+// 4 x 16-lane groups of ds_read_b128), and the stride-8 writes of the first
+// Stockham pass land on 8 distinct 16-byte bank groups (conflict-free for the
+// 8 x 8-lane groups of ds_write_b128).  An 8192-point transform therefore takes
+// exactly 128 KiB of the 160 KiB LDS.
 //
-// Twiddles come from one global table W[m] = exp(-2*pi*i*m/16384), m < 16384
-// (L2/Infinity-cache resident); an N-point transform uses stride 16384/N.
-// All sizes and radices are compile-time, every pass is a full
-// load -> barrier -> store -> barrier round over the workgroup.
+// Twiddles: one 16-byte load per radix-R butterfly from a global table
+// W[m] = exp(-2*pi*i*m/16384) (L2 resident), the other R-2 powers by complex
+// multiplication (depth <= 3 products, a few ulp).  An N-point transform uses
+// table stride 16384/N.  All sizes and radices are compile-time.
 #pragma once
 #include <hip/hip_runtime.h>
 
@@ -17,7 +21,14 @@ namespace ldg {
 
 constexpr int TW_N = 16384;
 
-__device__ __forceinline__ constexpr int PAD(int i) { return i + (i >> 3); }
+__device__ __forceinline__ constexpr int SW(int i) { return i ^ ((i >> 3) & 7); }
+
+// Swizzled complex buffer in LDS.
+struct CBuf {
+  double2* p;
+  __device__ __forceinline__ double2& operator[](int i) const { return p[SW(i)]; }
+  __device__ __forceinline__ CBuf operator+(int off) const { return CBuf{p + off}; }   // off: multiple of 8
+};
 
 __device__ __forceinline__ double2 cadd(double2 a, double2 b) { return make_double2(a.x + b.x, a.y + b.y); }
 __device__ __forceinline__ double2 csub(double2 a, double2 b) { return make_double2(a.x - b.x, a.y - b.y); }
@@ -69,37 +80,54 @@ template <int R, bool INV> __device__ __forceinline__ void dftR(double2* v) {
   else dft2<INV>(v[0], v[1]);
 }
 
-__device__ __forceinline__ double2 twiddle(const double2* __restrict__ tw, int m, bool inv) {
-  double2 w = tw[m];
-  return inv ? conj2(w) : w;
+// v[r] *= w^r, r = 1..R-1, from w = W^st (conjugated for the inverse).
+template <int R, bool INV>
+__device__ __forceinline__ void twiddle_row(double2* v, const double2* __restrict__ tw, int m) {
+  double2 w1 = tw[m];
+  if (INV) w1 = conj2(w1);
+  v[1] = cmul(v[1], w1);
+  if constexpr (R >= 4) {
+    const double2 w2 = cmul(w1, w1);
+    const double2 w3 = cmul(w2, w1);
+    v[2] = cmul(v[2], w2);
+    v[3] = cmul(v[3], w3);
+    if constexpr (R == 8) {
+      const double2 w4 = cmul(w2, w2);
+      v[4] = cmul(v[4], w4);
+      v[5] = cmul(v[5], cmul(w4, w1));
+      v[6] = cmul(v[6], cmul(w3, w3));
+      v[7] = cmul(v[7], cmul(w4, w3));
+    }
+  }
 }
 
 // One Stockham pass of radix R over an N-point array using threads [0, T).
-// Threads >= T only take part in the two barriers.
+// Threads >= T only take part in the barrier.
 template <int N, int T, int R, bool INV>
-__device__ __forceinline__ void stockham_pass(double* re, double* im, int Ns, const double2* __restrict__ tw, int tid) {
+__device__ __forceinline__ void stockham_pass(CBuf x, int Ns, const double2* __restrict__ tw, int tid) {
   constexpr int NB = N / R;                       // butterflies in this pass
   constexpr int BPT = NB >= T ? NB / T : 1;       // butterflies per active thread
   constexpr int TA = NB >= T ? T : NB;            // active threads
   constexpr int TWS = TW_N / N;
   double2 v[BPT][R];
+  // Launder tid per pass: the LDS addresses depend only on tid and constants,
+  // and without this the compiler hoists every pass's addresses of every
+  // transform in the kernel to its start (and spills them).
+  asm volatile("" : "+v"(tid));
   const bool act = tid < TA;
   if (act) {
 #pragma unroll
     for (int b = 0; b < BPT; b++) {
       const int j = tid + b * TA;
 #pragma unroll
-      for (int r = 0; r < R; r++) { const int i = PAD(j + r * NB); v[b][r] = make_double2(re[i], im[i]); }
+      for (int r = 0; r < R; r++) v[b][r] = x[j + r * NB];
       const int k = j & (Ns - 1);
-      if (Ns > 1) {
-        const int st = (N / (Ns * R)) * k;
-#pragma unroll
-        for (int r = 1; r < R; r++) v[b][r] = cmul(v[b][r], twiddle(tw, r * st * TWS, INV));
-      }
+      if (Ns > 1) twiddle_row<R, INV>(v[b], tw, (N / (Ns * R)) * k * TWS);
       dftR<R, INV>(v[b]);
     }
   }
   __syncthreads();
+  asm volatile("" : "+v"(tid));
   if (act) {
 #pragma unroll
     for (int b = 0; b < BPT; b++) {
@@ -107,7 +135,7 @@ __device__ __forceinline__ void stockham_pass(double* re, double* im, int Ns, co
       const int k = j & (Ns - 1);
       const int base = (j - k) * R + k;
 #pragma unroll
-      for (int r = 0; r < R; r++) { const int i = PAD(base + r * Ns); re[i] = v[b][r].x; im[i] = v[b][r].y; }
+      for (int r = 0; r < R; r++) x[base + r * Ns] = v[b][r];
     }
   }
   __syncthreads();
@@ -117,16 +145,16 @@ template <int N> struct Log2 { static constexpr int v = 1 + Log2<N / 2>::v; };
 template <> struct Log2<1> { static constexpr int v = 0; };
 
 // In-place N-point FFT (unnormalised), natural order in and out.  Begins with a
-// barrier so callers may write the input right before calling.
+// barrier so callers may write the input right before calling; ends with one.
 template <int N, int T, bool INV>
-__device__ __forceinline__ void fft_lds(double* re, double* im, const double2* __restrict__ tw, int tid) {
+__device__ __forceinline__ void fft_lds(CBuf x, const double2* __restrict__ tw, int tid) {
   __syncthreads();
   constexpr int L = Log2<N>::v;
   int Ns = 1;
 #pragma unroll
-  for (int p = 0; p < L / 3; p++) { stockham_pass<N, T, 8, INV>(re, im, Ns, tw, tid); Ns *= 8; }
-  if constexpr (L % 3 == 1) stockham_pass<N, T, 2, INV>(re, im, Ns, tw, tid);
-  if constexpr (L % 3 == 2) stockham_pass<N, T, 4, INV>(re, im, Ns, tw, tid);
+  for (int p = 0; p < L / 3; p++) { stockham_pass<N, T, 8, INV>(x, Ns, tw, tid); Ns *= 8; }
+  if constexpr (L % 3 == 1) stockham_pass<N, T, 2, INV>(x, Ns, tw, tid);
+  if constexpr (L % 3 == 2) stockham_pass<N, T, 4, INV>(x, Ns, tw, tid);
 }
 
 }  // namespace ldg

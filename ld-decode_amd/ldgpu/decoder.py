@@ -282,6 +282,18 @@ class GPUDecoder:
                 self.hints.pop(s, None)
             self._hint_keys = self._hint_keys[-2048:]
 
+    def _note_miss(self, key):
+        """Diagnostics: how far the nearest decoded read was from the one the replay needed."""
+        self.stats['misses'] = self.stats.get('misses', 0) + 1
+        best = None
+        for (s, m) in self.cache:
+            d = s - key[0]
+            if abs(d) <= 200000 and (best is None or abs(d) < abs(best[0])):
+                best = (d, m == key[1])
+        h = self.stats.setdefault('miss_log', [])
+        if len(h) < 64:
+            h.append(best)
+
     # ---- reference control flow --------------------------------------------------
     def _get(self, readsample, mtf, audio_offset):
         key = (int(readsample), mtf)
@@ -402,7 +414,8 @@ class GPUDecoder:
                 self.field_log = []
                 try:
                     fr = self.readframe(nextsample, (done + len(frames)) == 0)
-                except Miss:
+                except Miss as m:
+                    self._note_miss(m.key)
                     (nextsample, self.mtf_level, self.audio_offset, self.last_framenr, self.last_isclv,
                      self.last_read) = cp
                     break
