@@ -20,6 +20,9 @@ using namespace ldg;
 
 namespace {
 
+constexpr int SEG_K = 64;      // walk segments per read
+constexpr int SEG_NMAX = 96;   // visited positions recorded per segment
+
 struct SyncView {
   const int32_t* pk;   // peak positions
   const double* lv;    // ds[pk[i]]
@@ -40,7 +43,103 @@ struct SyncView {
   }
 };
 
+// First-occurrence argmax of ds[i, wend) with numpy semantics (a NaN is the
+// maximum; the first NaN wins), one wave: 20 coalesced loads per lane issued
+// back to back, then a cross-lane reduction.  Window <= 1280 samples.
+constexpr int ARGMAX_PER = 20;
+__device__ __forceinline__ bool am_beats(double v, int64_t vi, double b, int64_t bi) {
+  const bool vn = v != v, bn = b != b;
+  if (vn || bn) return vn && (!bn || vi < bi);
+  return v > b || (v == b && vi < bi);
+}
+__device__ inline void wave_argmax(const double* __restrict__ ds, int64_t i, int64_t wend, int lane, double& best,
+                                   int64_t& bidx) {
+  double vv[ARGMAX_PER];
+#pragma unroll
+  for (int q = 0; q < ARGMAX_PER; q++) {
+    const int64_t k = i + lane + 64 * q;
+    vv[q] = (k < wend) ? ds[k] : -__builtin_inf();
+  }
+  best = -__builtin_inf();
+  bidx = 0x7fffffffffffffffLL;
+#pragma unroll
+  for (int q = 0; q < ARGMAX_PER; q++)
+    if (am_beats(vv[q], i + lane + 64 * q, best, bidx)) { best = vv[q]; bidx = i + lane + 64 * q; }
+  for (int o = 32; o > 0; o >>= 1) {
+    const double ov = __shfl_xor(best, o);
+    const int64_t oi = __shfl_xor(bidx, o);
+    if (am_beats(ov, oi, best, bidx)) { best = ov; bidx = oi; }
+  }
+}
+
+// get_syncpeaks walk geometry for one read (lddecode_core.py:497-515).
+struct WalkGeom {
+  int64_t len, stop, seg;
+  int win, jump, ov;
+  __device__ WalkGeom(int64_t n_out, int linelen) {
+    len = n_out;
+    win = linelen / 2;                     // inlinelen // 2 (and the no-peak step linelen // 2)
+    jump = (int)((double)linelen * .4);    // int(rf.linelen * .4)
+    stop = len - 2 * (int64_t)linelen;
+    seg = stop > 0 ? (stop + SEG_K - 1) / SEG_K : 0;
+    ov = 4 * linelen;                      // a walker runs this far into the next segment
+  }
+};
+
+// binary search of p in the ascending list a[0..n): index or -1
+__device__ __forceinline__ int find_sorted(const int32_t* a, int n, int64_t p) {
+  int lo = 0, hi = n;
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if (a[mid] < p) lo = mid + 1; else hi = mid;
+  }
+  return (lo < n && a[lo] == p) ? lo : -1;
+}
+
 }  // namespace
+
+// ---------------------------------------------------------------------------
+// get_syncpeaks, part 1: the walk is a chain i -> next(i) (window argmax at i,
+// then bidx + jump or i + win).  Each read is cut into SEG_K segments and one
+// wave per segment walks the chain from the segment start to OV samples past
+// the next segment's start, recording every visited position.  Chains that
+// share a position coincide from there on (next() is a function of i alone),
+// so ldg_k_sync stitches the reference's exact walk from these lists.
+// grid: n_reads * SEG_K workgroups of 64 threads.
+extern "C" __global__ __launch_bounds__(64) void ldg_k_sync_walk(
+    const int32_t* __restrict__ smap, const ReadDesc* __restrict__ reads, const double* __restrict__ video,
+    int64_t vread_stride, int64_t vchan_stride, SysConst C, const int32_t* __restrict__ status,
+    int32_t* __restrict__ node_pos, int32_t* __restrict__ node_pk, double* __restrict__ node_lv,
+    int32_t* __restrict__ node_n) {
+  const int lane = threadIdx.x;
+  const int slot = smap[blockIdx.x / SEG_K];
+  const int k = blockIdx.x % SEG_K;
+  const int64_t L = (int64_t)slot * SEG_K + k;
+  if (status[slot] == FS_EOF) {
+    if (lane == 0) node_n[L] = 0;
+    return;
+  }
+  const ReadDesc rd = reads[slot];
+  const WalkGeom G(rd.n_out, C.linelen);
+  const double* ds = video + (int64_t)slot * vread_stride + (int64_t)CH_SYNC * vchan_stride;
+  int64_t i = (int64_t)k * G.seg;
+  int64_t e = (k == SEG_K - 1) ? G.stop : (int64_t)(k + 1) * G.seg + G.ov;
+  if (e > G.stop) e = G.stop;
+  int n = 0;
+  int32_t* P = node_pos + L * SEG_NMAX;
+  int32_t* K = node_pk + L * SEG_NMAX;
+  double* V = node_lv + L * SEG_NMAX;
+  while (i < e && n < SEG_NMAX) {
+    double best;
+    int64_t bidx;
+    wave_argmax(ds, i, i + G.win, lane, best, bidx);
+    const bool pk = best > .2;
+    if (lane == 0) { P[n] = (int32_t)i; K[n] = pk ? (int32_t)bidx : -1; V[n] = best; }
+    n++;
+    i = pk ? bidx + G.jump : i + G.win;
+  }
+  if (lane == 0) node_n[L] = n;
+}
 
 // ---------------------------------------------------------------------------
 // Sync peaks, hsync median/tolerance, vsyncs and the Field.__init__ branch.
@@ -48,10 +147,17 @@ struct SyncView {
 extern "C" __global__ __launch_bounds__(64) void ldg_k_sync(
     const int32_t* __restrict__ smap, const ReadDesc* __restrict__ reads, const double* __restrict__ video, int64_t vread_stride,
     int64_t vchan_stride, SysConst C, FieldRec* __restrict__ recs, int32_t* __restrict__ peaks,
-    const int32_t* __restrict__ status) {
+    const int32_t* __restrict__ status, const int32_t* __restrict__ node_pos, const int32_t* __restrict__ node_pk,
+    const double* __restrict__ node_lv, const int32_t* __restrict__ node_n) {
+  __shared__ int32_t s_npos[SEG_K * SEG_NMAX];
+  __shared__ int32_t s_npk[SEG_K * SEG_NMAX];
+  __shared__ int32_t s_cnt[SEG_K];
   __shared__ int32_t s_pk[MAX_PEAKS];
   __shared__ double s_lv[MAX_PEAKS];
   __shared__ double s_tmp[2 * MAX_PEAKS];
+  __shared__ int32_t s_cand[MAX_PEAKS];
+  __shared__ int s_hist[256];
+  __shared__ double s_sd;
   const int lane = threadIdx.x;
   const int slot = smap[blockIdx.x];
   FieldRec* R = recs + slot;
@@ -64,45 +170,84 @@ extern "C" __global__ __launch_bounds__(64) void ldg_k_sync(
   const double* ds = video + (int64_t)slot * vread_stride + (int64_t)CH_SYNC * vchan_stride;
   const int64_t len = rd.n_out;
   const int linelen = C.linelen;
-  const int win = linelen / 2;                     // inlinelen // 2
-  const int jump = (int)((double)linelen * .4);    // int(rf.linelen * .4)
-  const int64_t stop = len - 2 * (int64_t)linelen;
+  const WalkGeom G(len, linelen);
 
-  // ---- get_syncpeaks: sequential window-argmax walk --------------------------
+  // ---- get_syncpeaks, part 2: stitch the segment chains ------------------------
+  for (int q = lane; q < SEG_K; q += 64) s_cnt[q] = node_n[(int64_t)slot * SEG_K + q];
+  for (int q = lane; q < SEG_K * SEG_NMAX; q += 64) {
+    s_npos[q] = node_pos[(int64_t)slot * SEG_K * SEG_NMAX + q];
+    s_npk[q] = node_pk[(int64_t)slot * SEG_K * SEG_NMAX + q];
+  }
+  __syncthreads();
+  const double* nlv = node_lv + (int64_t)slot * SEG_K * SEG_NMAX;
   int np = 0;
   bool overflow = false;
-  int64_t i = 0;
-  while (i < stop) {
-    const int64_t wend = (i + win < len) ? i + win : len;
-    double best = -__builtin_inf();
-    int64_t bidx = 0x7fffffffffffffffLL;
-    // all of this lane's window loads issued back to back, then a first-occurrence max
-    constexpr int PER = 20;                         // ceil(1280 / 64): PAL window 1280, NTSC 1271
-    double vv[PER];
-#pragma unroll
-    for (int q = 0; q < PER; q++) {
-      const int64_t k = i + lane + 64 * q;
-      vv[q] = (k < wend) ? ds[k] : -__builtin_inf();
+  // append path nodes [a, b) of chain k (their peaks, in order)
+  auto emit = [&](int k, int a, int b) {
+    for (int j0 = a; j0 < b && !overflow; j0 += 64) {
+      const int j = j0 + lane;
+      const bool isp = j < b && s_npk[k * SEG_NMAX + j] >= 0;
+      const uint64_t m = __ballot(isp);
+      const int rank = __popcll(m & ((1ull << lane) - 1ull));
+      const int tot = __popcll(m);
+      if (np + tot > MAX_PEAKS) { overflow = true; break; }
+      if (isp) { s_pk[np + rank] = s_npk[k * SEG_NMAX + j]; s_lv[np + rank] = nlv[k * SEG_NMAX + j]; }
+      np += tot;
     }
-#pragma unroll
-    for (int q = 0; q < PER; q++)
-      if (vv[q] > best) { best = vv[q]; bidx = i + lane + 64 * q; }
-    for (int o = 32; o > 0; o >>= 1) {
-      const double ov = __shfl_xor(best, o);
-      const int64_t oi = __shfl_xor(bidx, o);
-      if (ov > best || (ov == best && oi < bidx)) { best = ov; bidx = oi; }
-    }
-    if (best > .2) {
-      if (np < MAX_PEAKS) {
-        if (lane == 0) { s_pk[np] = (int32_t)bidx; s_lv[np] = best; }
-        np++;
-      } else {
-        overflow = true;
-        break;
+  };
+  if (G.stop > 0) {
+    int k = 0, a = 0;
+    while (!overflow) {
+      const int cnt = s_cnt[k];
+      const int32_t* pos = s_npos + k * SEG_NMAX;
+      // b: first node j >= a of chain k that chain k+1 also visits
+      int b = -1, jn = -1;
+      if (k + 1 < SEG_K && s_cnt[k + 1] > 0) {
+        const int32_t* pn = s_npos + (k + 1) * SEG_NMAX;
+        for (int j0 = a; j0 < cnt && b < 0; j0 += 64) {
+          const int j = j0 + lane;
+          const int f = (j < cnt) ? find_sorted(pn, s_cnt[k + 1], pos[j]) : -1;
+          const uint64_t m = __ballot(f >= 0);
+          if (m) {
+            const int src = __ffsll((unsigned long long)m) - 1;
+            b = j0 + src;
+            jn = __shfl(f, src);
+          }
+        }
       }
-      i = bidx + jump;
-    } else {
-      i += win;
+      if (b >= 0) {
+        emit(k, a, b);
+        k += 1; a = jn;
+        continue;
+      }
+      emit(k, a, cnt);
+      if (overflow || cnt == 0) break;
+      // chain k ended without meeting chain k+1: walk on directly until the
+      // path lands on a position some later chain visits (or the walk ends)
+      const int last = k * SEG_NMAX + cnt - 1;
+      int64_t p = s_npk[last] >= 0 ? (int64_t)s_npk[last] + G.jump : (int64_t)s_npos[last] + G.win;
+      bool joined = false;
+      while (p < G.stop && !overflow) {
+        for (int j = k + 1; j < SEG_K && !joined; j++) {
+          const int c = s_cnt[j];
+          if (c == 0 || s_npos[j * SEG_NMAX] > p || s_npos[j * SEG_NMAX + c - 1] < p) continue;
+          const int f = find_sorted(s_npos + j * SEG_NMAX, c, p);
+          if (f >= 0) { k = j; a = f; joined = true; }
+        }
+        if (joined) break;
+        double best;
+        int64_t bidx;
+        wave_argmax(ds, p, p + G.win, lane, best, bidx);
+        if (best > .2) {
+          if (np >= MAX_PEAKS) { overflow = true; break; }
+          if (lane == 0) { s_pk[np] = (int32_t)bidx; s_lv[np] = best; }
+          np++;
+          p = bidx + G.jump;
+        } else {
+          p += G.win;
+        }
+      }
+      if (!joined) break;
     }
   }
   __syncthreads();
@@ -112,39 +257,55 @@ extern "C" __global__ __launch_bounds__(64) void ldg_k_sync(
     if (lane == 0) { R->status = FS_CRASH; R->nvsync = 0; }
     return;
   }
-  if (lane != 0) return;
-
-  // ---- determine_vsyncs (lane 0) ---------------------------------------------
-  R->nvsync = 0;
-  R->status = FS_PENDING;
+  // ---- determine_vsyncs -------------------------------------------------------
   int64_t vs[MAX_VSYNCS][3];
   int nf = 0;
   double med = 0, tol = 0;
   bool err = false;
+  if (lane == 0) { R->nvsync = 0; R->status = FS_PENDING; }
+  int ncand = 0;
   if (np >= 200) {
+    // get_hsync_median: the in-range levels in peak order (compacted by ballot)
     int nh = 0;
-    for (int k = 0; k < np; k++)
-      if (inrange(s_lv[k], 0.6, 0.8)) s_tmp[nh++] = s_lv[k];
-    // np.std over the list in peak order, then np.median (sorts a copy)
-    double sd;
+    for (int j0 = 0; j0 < np; j0 += 64) {
+      const int j = j0 + lane;
+      const bool ok = j < np && inrange(s_lv[j], 0.6, 0.8);
+      const uint64_t m = __ballot(ok);
+      if (ok) s_tmp[nh + __popcll(m & ((1ull << lane) - 1ull))] = s_lv[j];
+      nh += __popcll(m);
+    }
+    __syncthreads();
+    // np.median: the middle order statistic(s), by radix select
     if (nh > 0) {
-      double* sq = s_tmp + nh;                       // scratch after the levels
-      sd = np_std(s_tmp, nh, sq);
-      isort(s_tmp, nh);
-      med = sorted_median(s_tmp, nh);
+      med = (nh & 1) ? wave_kth(s_tmp, nh, nh / 2, lane, s_hist)
+                     : (wave_kth(s_tmp, nh, nh / 2 - 1, lane, s_hist) + wave_kth(s_tmp, nh, nh / 2, lane, s_hist)) / 2.0;
     } else {
-      sd = __builtin_nan("");
       med = __builtin_nan("");
     }
+    // np.std over the list in peak order (numpy pairwise order, lane 0)
+    if (lane == 0) s_sd = nh > 0 ? np_std(s_tmp, nh, s_tmp + nh) : __builtin_nan("");
+    __syncthreads();
+    const double sd = s_sd;
     const double t2 = sd * 2;
     tol = (.01 > t2) ? .01 : t2;                     // Python max(t2, .01): keeps t2 unless .01 > t2
+    // vsync candidates: peak > .9 after a peak below med - 2 tol
+    for (int j0 = 0; j0 < np; j0 += 64) {
+      const int j = j0 + lane;
+      const bool c = j < np && s_lv[j] > .9 && (j ? s_lv[j - 1] : 1.0) < med - (tol * 2);
+      const uint64_t m = __ballot(c);
+      if (c) s_cand[ncand + __popcll(m & ((1ull << lane) - 1ull))] = j;
+      ncand += __popcll(m);
+    }
+    __syncthreads();
+  }
+  if (lane != 0) return;
+  if (np >= 200) {
     R->med_hsync = med;
     R->hsync_tol = tol;
     SyncView V{s_pk, s_lv, np, med, tol};
-    double prev = 1.0;
-    for (int k = 0; k < np; k++) {
-      const double lvl = s_lv[k];
-      if (lvl > .9 && prev < med - (tol * 2)) {
+    for (int ci = 0; ci < ncand; ci++) {
+      const int k = s_cand[ci];
+      {
         if (k < 11) { R->status = FS_CRASH; return; }     // determine_field -> None, unpacked
         // determine_field (lddecode_core.py:544-588)
         int vote = 0;
@@ -174,7 +335,6 @@ extern "C" __global__ __launch_bounds__(64) void ldg_k_sync(
           nf++;
         }
       }
-      prev = lvl;
     }
     if (nf >= 2) {
       // vote repair + line0 override + bool conversion, in place like the numpy array va

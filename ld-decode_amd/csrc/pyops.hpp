@@ -120,6 +120,50 @@ __device__ inline double np_median(const double* a, int n, double* tmp) {
   return sorted_median(tmp, n);
 }
 
+// k-th smallest (0-based) of a[0..n) for non-negative, non-NaN doubles, one
+// wave (all 64 lanes call it): radix select over the IEEE bit patterns (which
+// order like the values for x >= 0), 8 bits per pass.  hist: 256 ints of LDS.
+__device__ inline double wave_kth(const double* a, int n, int k, int lane, int* hist) {
+  uint64_t prefix = 0, mask = 0;
+  for (int shift = 56; shift >= 0; shift -= 8) {
+    for (int d = lane; d < 256; d += 64) hist[d] = 0;
+    __syncthreads();
+    for (int i = lane; i < n; i += 64) {
+      const uint64_t u = (uint64_t)__double_as_longlong(a[i]);
+      if ((u & mask) == prefix) atomicAdd(&hist[(u >> shift) & 255], 1);
+    }
+    __syncthreads();
+    // digit whose cumulative count passes k: lane owns digits 4*lane..4*lane+3
+    int c[4], tot = 0;
+#pragma unroll
+    for (int e = 0; e < 4; e++) { c[e] = hist[4 * lane + e]; tot += c[e]; }
+    int incl = tot;
+    for (int o = 1; o < 64; o <<= 1) {
+      const int v = __shfl_up(incl, o);
+      if (lane >= o) incl += v;
+    }
+    const int excl = incl - tot;
+    int digit = -1, below = 0;
+    if (k >= excl && k < incl) {
+      int run = excl;
+#pragma unroll
+      for (int e = 0; e < 4; e++) {
+        if (digit < 0 && k < run + c[e]) { digit = 4 * lane + e; below = run; }
+        run += c[e];
+      }
+    }
+    const uint64_t m = __ballot(digit >= 0);
+    const int src = __ffsll((unsigned long long)m) - 1;
+    digit = __shfl(digit, src);
+    below = __shfl(below, src);
+    k -= below;
+    prefix |= (uint64_t)digit << shift;
+    mask |= (uint64_t)255 << shift;
+    __syncthreads();
+  }
+  return __longlong_as_double((long long)prefix);
+}
+
 // Block-wide bitonic sort of a[0..npow2) in LDS (npow2 a power of two, pad with +inf).
 __device__ inline void block_bitonic_sort(double* a, int npow2, int tid, int nthreads) {
   for (int k = 2; k <= npow2; k <<= 1) {
