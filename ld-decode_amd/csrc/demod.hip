@@ -418,9 +418,12 @@ extern "C" __global__ __launch_bounds__(1024) void ldg_k_audio2(
 // exp(m*log|MTF|) * cis(m*arg MTF) (cpow = cexp(m*clog)).  m == 0: RFVideo.
 extern "C" __global__ void ldg_k_rf_table(const double2* __restrict__ rfvideo, const double2* __restrict__ mtf,
                                            const double* __restrict__ mtf_logabs, const double* __restrict__ mtf_arg,
-                                           double m, double2* __restrict__ out) {
+                                           const double* __restrict__ mtfs, double2* __restrict__ tables) {
+  // grid: (BLOCKLEN / 256, n_tables); table y has mtf level mtfs[y]
   const int k = blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= BLOCKLEN) return;
+  const double m = mtfs[blockIdx.y];
+  double2* out = tables + (size_t)blockIdx.y * BLOCKLEN;
   const double2 r = rfvideo[k];
   double2 p;
   if (m == 0.0) { out[k] = r; return; }

@@ -390,26 +390,27 @@ extern "C" __global__ __launch_bounds__(64) void ldg_k_linelocs(
   __shared__ uint8_t s_has[LINENUM_SPAN];
   __shared__ uint8_t s_orig[LINENUM_SPAN];
   __shared__ double s_lv[MAX_PEAKS];
+  __shared__ int32_t s_pkl[MAX_PEAKS];
+  __shared__ double win[25];         // sorted window of the last 25 accepted line lengths
+  __shared__ double ring[25];        // the same values in arrival order
   const int lane = threadIdx.x;
   const int slot = smap[blockIdx.x];
   FieldRec* R = recs + slot;
   if (R->status != FS_PENDING) return;
   const int np = R->npeaks;
-  const int32_t* pk = peaks + (int64_t)slot * MAX_PEAKS;
+  const int32_t* pkg = peaks + (int64_t)slot * MAX_PEAKS;
   const double* ds = video + (int64_t)slot * vread_stride + (int64_t)CH_SYNC * vchan_stride;
   for (int k = lane; k < LINENUM_SPAN; k += 64) { s_has[k] = 0; s_orig[k] = 0; }
-  for (int k = lane; k < np; k += 64) s_lv[k] = ds[pk[k]];
+  for (int k = lane; k < np; k += 64) { const int32_t p = pkg[k]; s_pkl[k] = p; s_lv[k] = ds[p]; }
   __syncthreads();
   if (lane != 0) return;
+  const int32_t* pk = s_pkl;
 
   const double inl = (double)C.linelen;
   SyncView V{pk, s_lv, np, R->med_hsync, R->hsync_tol};
   const int64_t v01 = R->vsync[0][1], v11 = R->vsync[1][1];
   const int linecount = R->linecount;
   bool err = false;
-  // sliding window of the last 25 accepted line lengths, kept sorted
-  double win[25];
-  double ring[25];
   int nlens = 1, rpos = 0;
   win[0] = inl; ring[0] = inl;
   int64_t prev_idx = -1, prev_num = 0;

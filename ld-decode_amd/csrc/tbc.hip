@@ -7,12 +7,12 @@
 // (:1023-1035), downscale_audio (:431-484) and Framer.formatoutput (:1238-1252).
 //
 // Spline: scipy splrep(s=0) on unit-spaced points is the not-a-knot cubic
-// interpolant; it is solved in second-derivative form with a Thomas sweep over
-// a window of rows reaching KTR=40 samples past the outputs a lane produces
-// (exact to rho^40 ~ 1e-23 relative, below double rounding).  The burst pass
-// runs one lane per line (40 outputs, ~100-row windows); the final pass splits
-// each line over 8 lanes.  The Thomas scratch is lane-interleaved
-// (dp[t*64 + lane]) so every step is a coalesced 512-byte access.
+// interpolant, solved in second-derivative form.  The burst pass (40 outputs
+// per line) runs one lane per line with a Thomas sweep over a window of rows
+// reaching KTR=40 samples past its outputs (exact to rho^40 ~ 1e-23 relative,
+// below double rounding; lane-interleaved scratch dp[t*64 + lane], coalesced).
+// The final pass runs one wave per line with the line in LDS and the
+// tridiagonal solve as chunked affine scans (spline_line_wave).
 #include <hip/hip_runtime.h>
 #include "common.hpp"
 #include "field_rec.hpp"
@@ -24,8 +24,6 @@ namespace {
 
 constexpr int SPL_MAXN = 2816;                 // max points per line (NTSC ~2545, PAL ~2563)
 constexpr int LINE_GROUPS = (MAX_LINES + 63) / 64;
-constexpr int FSEG = 8;                        // final pass: lanes per line
-constexpr int FGROUPS = MAX_LINES / (64 / FSEG); // final pass: workgroups per read
 
 struct CTab { double v[17]; };
 constexpr CTab make_ctab() {
@@ -43,7 +41,7 @@ __device__ __forceinline__ double ctab(int64_t t) { return g_ctab.v[t < 16 ? t :
 // the result by < rho^KTR ~ 1.5e-23 (relative) -- below double rounding.
 constexpr int KTR = 40;
 constexpr int SCR_LANE = 512;                 // Thomas scratch entries per lane
-constexpr int64_t SCR_PER_SLOT = (int64_t)FGROUPS * 64 * SCR_LANE;
+constexpr int64_t SCR_PER_SLOT = (int64_t)LINE_GROUPS * 64 * SCR_LANE;   // burst pass
 
 // Not-a-knot cubic spline through y[j] = buf[ib + j], j = 0..n (lddutils.scale:
 // splrep(s=0) on unit spacing), evaluated at x_o = o*step + x0 (numpy
@@ -118,6 +116,101 @@ __device__ int spline_window(const double* __restrict__ buf, int64_t len, double
     const double M2 = Mnext;
     if (jhi >= 1) emit(1, M1, M2, jlo == 1);
     if (o >= o_lo) emit(0, 2.0 * M1 - M2, M1, true);
+  }
+  return 0;
+}
+
+// The same interpolant for a whole line on one wave, outputs o = lane + 64 q.
+// The line's samples go to LDS (ys) with one coalesced load; the tridiagonal
+// solve for M_2..M_{n-2} runs as chunked affine scans: lane l owns rows
+// [l*CH, (l+1)*CH) (CH odd: conflict-free strided LDS access), composes its
+// rows' maps, a 64-lane Kogge-Stone scan yields each chunk's carry-in, and the
+// lane re-runs its rows with the Thomas arithmetic (forward d_t = (r_t -
+// d_{t-1}) c_t, backward M_t = d_t - c_t M_{t+1}) into ms.  Returns -1 (wave
+// uniform) where splrep would raise.
+template <class Sink>
+__device__ int spline_line_wave(const double* __restrict__ buf, int64_t len, double begin, double end, int W, int lane,
+                                double* __restrict__ ys, double* __restrict__ ms, double* __restrict__ ct, Sink&& sink) {
+  // c'_t table in LDS: the row index differs per lane, and a per-lane index
+  // into __constant__ memory is a vector memory load on the recurrence path
+  if (lane < 17) ct[lane] = g_ctab.v[lane];
+  auto ctab = [&](int t) { return ct[t < 16 ? t : 16]; };
+  const int64_t ib = py_int(begin), ie = py_int(end);
+  const int64_t n64 = ie - ib;
+  if (ib < 0 || n64 < 6 || n64 >= SPL_MAXN || ib + n64 + 1 > len) return -1;
+  const int n = (int)n64;
+  const double* y = buf + ib;
+  for (int j = lane; j <= n; j += 64) ys[j] = y[j];
+  __syncthreads();
+  auto rr = [&](int j) { return 6.0 * ((ys[j + 1] - ys[j]) - (ys[j] - ys[j - 1])); };
+  const double M1 = rr(1) / 6.0, Mn1 = rr(n - 1) / 6.0;
+  const int T = n - 3;                                // rows j = t + 2, t in [0, T)
+  int CH = (T + 63) / 64;
+  CH |= 1;
+  const int t0 = lane * CH;
+  const int t1 = (t0 + CH < T) ? t0 + CH : T;
+  auto rhs = [&](int t) {
+    double r = rr(t + 2);
+    if (t == 0) r -= M1;
+    if (t == T - 1) r -= Mn1;
+    return r;
+  };
+  // forward: compose d -> -c d + c r over my rows
+  double A = 1.0, B = 0.0;
+  for (int t = t0; t < t1; t++) {
+    const double c = ctab(t);
+    A = -c * A;
+    B = (rhs(t) - B) * c;
+  }
+  for (int o = 1; o < 64; o <<= 1) {                   // inclusive scan of (A, B) over lanes
+    const double pa = __shfl_up(A, o), pb = __shfl_up(B, o);
+    if (lane >= o) { B = A * pb + B; A = A * pa; }
+  }
+  double dprev = __shfl_up(B, 1);
+  if (lane == 0) dprev = 0.0;
+  for (int t = t0; t < t1; t++) {
+    const double d = (rhs(t) - dprev) * ctab(t);
+    ms[t + 2] = d;
+    dprev = d;
+  }
+  // backward: compose M -> d - c M over my rows, top down
+  A = 1.0; B = 0.0;
+  for (int t = t1 - 1; t >= t0; t--) {
+    const double c = ctab(t);
+    A = -c * A;
+    B = ms[t + 2] - c * B;
+  }
+  for (int o = 1; o < 64; o <<= 1) {                   // inclusive suffix scan over lanes
+    const double pa = __shfl_down(A, o), pb = __shfl_down(B, o);
+    if (lane + o < 64) { B = A * pb + B; A = A * pa; }
+  }
+  double Mnext = __shfl_down(B, 1);
+  if (lane == 63) Mnext = 0.0;
+  for (int t = t1 - 1; t >= t0; t--) {
+    const double M = ms[t + 2] - ctab(t) * Mnext;
+    ms[t + 2] = M;
+    Mnext = M;
+  }
+  __syncthreads();
+  if (lane == 0) {
+    ms[1] = M1;
+    ms[0] = 2.0 * M1 - ms[2];
+    ms[n - 1] = Mn1;
+    ms[n] = 2.0 * Mn1 - ms[n - 2];
+  }
+  __syncthreads();
+  const double x0 = begin - (double)ib;
+  const double span = end - begin;
+  const double step = ((span + x0) - x0) / (double)W;
+  for (int o = lane; o < W; o += 64) {
+    double x = (double)o * step;
+    x = x + x0;
+    int64_t k = (int64_t)floor(x);
+    k = k < 0 ? 0 : (k > n - 1 ? n - 1 : k);
+    const double Mk = ms[k], Mk1 = ms[k + 1], yk = ys[k], yk1 = ys[k + 1];
+    const double a = (double)(k + 1) - x, b = x - (double)k;
+    const double v = Mk * a * a * a / 6.0 + Mk1 * b * b * b / 6.0 + (yk - Mk / 6.0) * a + (yk1 - Mk1 / 6.0) * b;
+    sink(o, v);
   }
   return 0;
 }
@@ -317,21 +410,21 @@ extern "C" __global__ __launch_bounds__(64) void ldg_k_burst_field(const int32_t
 extern "C" __global__ __launch_bounds__(64) void ldg_k_final_lines(
     const int32_t* __restrict__ smap, const double* __restrict__ video, int64_t vread_stride, int64_t vchan_stride,
     SysConst C, FieldRec* __restrict__ recs, const double* __restrict__ lines, const float* __restrict__ blevel,
-    double* __restrict__ scratch, uint16_t* __restrict__ pic, int64_t pic_stride) {
+    uint16_t* __restrict__ pic, int64_t pic_stride) {
+  __shared__ double s_y[SPL_MAXN + 1];
+  __shared__ double s_m[SPL_MAXN + 1];
+  __shared__ double s_ct[17];
   const int lane = threadIdx.x;
-  const int slot = smap[blockIdx.x / FGROUPS];
-  const int grp = blockIdx.x % FGROUPS;
+  const int slot = smap[blockIdx.x / MAX_LINES];
+  const int row = blockIdx.x % MAX_LINES;
   FieldRec* R = recs + slot;
   if (R->status != FS_PENDING) return;
-  const int row = grp * (64 / FSEG) + lane / FSEG;   // FSEG lanes share one output line
-  const int seg = lane % FSEG;
   const int lc = R->linecount;
   if (row >= lc) return;
   const int loff = (C.system == 1) ? 3 : 1;
   const int l = row + loff;
   const double* lf = lines + (int64_t)slot * LINES_STRIDE + LLF * MAX_LINES;
   const double* dm = video + (int64_t)slot * vread_stride + (int64_t)CH_DEMOD * vchan_stride;
-  double* dp = scratch + (int64_t)slot * SCR_PER_SLOT + (int64_t)grp * 64 * SCR_LANE + lane;
   const int W = C.outlinelen;
   uint16_t* out = pic + (int64_t)slot * pic_stride + (int64_t)row * W;
   const double b0 = lf[l], b1 = lf[l + 1];
@@ -340,8 +433,7 @@ extern "C" __global__ __launch_bounds__(64) void ldg_k_final_lines(
   const double scale_ = pal ? (double)(0xd300 - 0x0100) / (100 - C.vsync_ire)
                             : (double)(0xc800 - 0x0400) / (100 - C.vsync_ire);
   const double base = pal ? 256.0 : 1024.0;
-  const int o_lo = seg * W / FSEG, o_hi = (seg + 1) * W / FSEG;
-  const int rc = spline_window<64>(dm, R->n_out, b0, b1, W, o_lo, o_hi, dp, [&](int o, double v) {
+  const int rc = spline_line_wave(dm, R->n_out, b0, b1, W, lane, s_y, s_m, s_ct, [&](int o, double v) {
     double red = ((v * wow) - C.ire0) / C.hz_ire;
     red -= C.vsync_ire;
     double x = (red * scale_) + base;
@@ -349,13 +441,17 @@ extern "C" __global__ __launch_bounds__(64) void ldg_k_final_lines(
     x = fmin(fmax(x, 0.0), 65535.0) + 0.5;
     out[o] = (uint16_t)x;
   });
-  if (rc < 0) { R->status = FS_TBC; return; }
-  if (!pal && seg == 0 && row >= 1 && row < lc - 1) {
+  if (rc < 0) {
+    if (lane == 0) R->status = FS_TBC;
+    return;
+  }
+  // NTSC burst flag pixels (lanes 0 / 1 wrote pixels 0 / 1 above)
+  if (!pal && lane < 2 && row >= 1 && row < lc - 1) {
     const float bl = blevel[(int64_t)slot * MAX_LINES + row];
     const double hzs = 1700000 / 140.0;
-    out[0] = bl > 0 ? 16384 : 32768;
+    if (lane == 0) out[0] = bl > 0 ? 16384 : 32768;
     const double clevel = (1 / 1.45) / hzs;
-    out[1] = (uint16_t)(327.67 * clevel * fabs((double)bl));
+    if (lane == 1) out[1] = (uint16_t)(327.67 * clevel * fabs((double)bl));
   }
 }
 
