@@ -381,7 +381,15 @@ extern "C" __global__ __launch_bounds__(64) void ldg_k_sync(
 }
 
 // ---------------------------------------------------------------------------
-// compute_linelocs (lddecode_core.py:638-713).  grid: n_reads x 64 threads; lane 0.
+// compute_linelocs (lddecode_core.py:638-713), one wave per read.
+// The reference's loop is a recurrence only through prevlinenum and the
+// window of the last 25 accepted line lengths; both are prefix quantities, so
+// it runs as: regular-peak compaction, accepted-gap compaction (ballots), the
+// running median only where a peak's gap is not accepted (rank counting over
+// <= 25 values), and a prefix sum of the line-number increments.  The gap
+// fill is parallel except the tail extrapolation past the last valid line,
+// which chains through earlier fills and stays sequential.
+// grid: n_reads workgroups of 64 threads.
 extern "C" __global__ __launch_bounds__(64) void ldg_k_linelocs(
     const int32_t* __restrict__ smap, const double* __restrict__ video, int64_t vread_stride, int64_t vchan_stride, SysConst C,
     FieldRec* __restrict__ recs, const int32_t* __restrict__ peaks, double* __restrict__ lines,
@@ -391,8 +399,11 @@ extern "C" __global__ __launch_bounds__(64) void ldg_k_linelocs(
   __shared__ uint8_t s_orig[LINENUM_SPAN];
   __shared__ double s_lv[MAX_PEAKS];
   __shared__ int32_t s_pkl[MAX_PEAKS];
-  __shared__ double win[25];         // sorted window of the last 25 accepted line lengths
-  __shared__ double ring[25];        // the same values in arrival order
+  __shared__ int32_t s_ridx[MAX_PEAKS];     // regular peaks, in order
+  __shared__ int32_t s_nb[MAX_PEAKS];       // accepted gaps before regular peak m; < 0: m's gap accepted
+  __shared__ int32_t s_num[MAX_PEAKS];      // line number of regular peak m
+  __shared__ double s_agap[MAX_PEAKS];      // accepted gaps, in order
+  __shared__ int s_flag;
   const int lane = threadIdx.x;
   const int slot = smap[blockIdx.x];
   FieldRec* R = recs + slot;
@@ -402,99 +413,250 @@ extern "C" __global__ __launch_bounds__(64) void ldg_k_linelocs(
   const double* ds = video + (int64_t)slot * vread_stride + (int64_t)CH_SYNC * vchan_stride;
   for (int k = lane; k < LINENUM_SPAN; k += 64) { s_has[k] = 0; s_orig[k] = 0; }
   for (int k = lane; k < np; k += 64) { const int32_t p = pkg[k]; s_pkl[k] = p; s_lv[k] = ds[p]; }
+  if (lane == 0) s_flag = 0;
   __syncthreads();
-  if (lane != 0) return;
   const int32_t* pk = s_pkl;
-
   const double inl = (double)C.linelen;
   SyncView V{pk, s_lv, np, R->med_hsync, R->hsync_tol};
-  const int64_t v01 = R->vsync[0][1], v11 = R->vsync[1][1];
+  const int v11 = R->vsync[1][1];
+  const int64_t v01 = R->vsync[0][1];
   const int linecount = R->linecount;
   bool err = false;
-  int nlens = 1, rpos = 0;
-  win[0] = inl; ring[0] = inl;
-  int64_t prev_idx = -1, prev_num = 0;
-  for (int64_t i = 0; i < v11; i++) {
-    const int wn = nlens < 25 ? nlens : 25;
-    const double med_len = sorted_median(win, wn);
-    if (V.regular(i, 0x7fffffffffffLL, err)) {
-      int64_t num;
-      if (prev_idx >= 0) {
-        const int64_t gap = (int64_t)pk[i] - pk[prev_idx];
-        if (inrange((double)gap / inl, .98, 1.02)) {
-          // lens.append(gap): update the sorted window of the last 25
-          const double g = (double)gap;
-          if (nlens >= 25) {
-            const double old = ring[rpos];
-            int p = 0;
-            while (p < 25 && win[p] != old) p++;
-            for (int q = p; q < 24; q++) win[q] = win[q + 1];
-            ring[rpos] = g; rpos = (rpos + 1) % 25;
-            int q = 23;
-            while (q >= 0 && win[q] > g) { win[q + 1] = win[q]; q--; }
-            win[q + 1] = g;
-          } else {
-            ring[nlens] = g;
-            int q = nlens - 1;
-            while (q >= 0 && win[q] > g) { win[q + 1] = win[q]; q--; }
-            win[q + 1] = g;
-            if (nlens + 1 == 25) rpos = 0;
-          }
-          nlens++;
-          num = prev_num + 1;
-        } else {
-          num = prev_num + (int64_t)np_round((double)(pk[i] - pk[prev_idx]) / med_len);
-        }
-      } else {
-        const int64_t base_peak = V.peak(v01, err);   // plist[vsyncs[0][1]], evaluated lazily
-        num = (int64_t)np_round((double)(pk[i] - base_peak) / med_len);
-      }
-      const int64_t key = num + LINENUM_OFF;
-      if (key < 0 || key >= LINENUM_SPAN) { R->status = FS_LINELOCS; return; }
-      s_key[key] = (double)pk[i];
-      s_has[key] = 1; s_orig[key] = 1;
-      prev_idx = i; prev_num = num;
+  // 1. regular hsync peaks among [0, vsyncs[1][1])
+  int nr = 0;
+  for (int i0 = 0; i0 < v11; i0 += 64) {
+    const int i = i0 + lane;
+    const bool r = i < v11 && V.regular(i, 0x7fffffffffffLL, err);
+    const uint64_t m = __ballot(r);
+    if (r) s_ridx[nr + __popcll(m & ((1ull << lane) - 1ull))] = i;
+    nr += __popcll(m);
+  }
+  __syncthreads();
+  // 2. accepted gaps (inrange(gap / inlinelen, .98, 1.02)) and their running count
+  int nacc = 0;
+  for (int m0 = 0; m0 < nr; m0 += 64) {
+    const int m = m0 + lane;
+    bool acc = false;
+    int64_t gap = 0;
+    if (m >= 1 && m < nr) {
+      gap = (int64_t)pk[s_ridx[m]] - pk[s_ridx[m - 1]];
+      acc = inrange((double)gap / inl, .98, 1.02);
+    }
+    const uint64_t msk = __ballot(acc);
+    const int rank = __popcll(msk & ((1ull << lane) - 1ull));
+    if (m < nr) s_nb[m] = acc ? -1 - (nacc + rank) : nacc + rank;
+    if (acc) s_agap[nacc + rank] = (double)gap;
+    nacc += __popcll(msk);
+  }
+  __syncthreads();
+  // 3. line-number increments; np.median(linelens[-25:]) only where it is used
+  int64_t base_peak = 0;
+  if (nr > 0) {
+    base_peak = V.peak(v01, err);       // plist[vsyncs[0][1]] (first regular peak's reference)
+    if (err) {
+      if (lane == 0) R->status = FS_CRASH;
+      return;
     }
   }
-  if (err) { R->status = FS_CRASH; return; }
-  // fill missing line numbers 1..linecount+4
-  double* L1 = lines + (int64_t)slot * LINES_STRIDE + LL1 * MAX_LINES;
-  int8_t* B1 = bad + (int64_t)slot * MAX_LINES;
-  for (int l = 1; l < linecount + 5; l++) {
+  for (int m0 = 0; m0 < nr; m0 += 64) {
+    const int m = m0 + lane;
+    if (m < nr) {
+      const int nbv = s_nb[m];
+      int inc;
+      if (nbv < 0) {
+        inc = 1;
+      } else {
+        // linelens = [inlinelen] + accepted gaps before m; median of the last 25
+        const int nl_ = 1 + nbv;
+        const int lo0 = nl_ > 25 ? nl_ - 25 : 0;
+        const int wn = nl_ - lo0;
+        auto L = [&](int q) { return q == 0 ? inl : s_agap[q - 1]; };
+        auto kth = [&](int r) {
+          for (int a = lo0; a < nl_; a++) {
+            const double va = L(a);
+            int lt = 0, le = 0;
+            for (int b2 = lo0; b2 < nl_; b2++) { const double vb = L(b2); lt += vb < va; le += vb <= va; }
+            if (lt <= r && r < le) return va;
+          }
+          return __builtin_nan("");
+        };
+        const double med = (wn & 1) ? kth(wn / 2) : (kth(wn / 2 - 1) + kth(wn / 2)) / 2.0;
+        const int64_t ref = (m == 0) ? base_peak : (int64_t)pk[s_ridx[m - 1]];
+        inc = (int)(int64_t)np_round((double)((int64_t)pk[s_ridx[m]] - ref) / med);
+      }
+      s_num[m] = inc;
+    }
+  }
+  __syncthreads();
+  // 4. inclusive prefix sum -> line numbers; dict assignment (last write wins)
+  int carry = 0;
+  for (int m0 = 0; m0 < nr; m0 += 64) {
+    const int m = m0 + lane;
+    int v = (m < nr) ? s_num[m] : 0;
+    for (int o = 1; o < 64; o <<= 1) {
+      const int t = __shfl_up(v, o);
+      if (lane >= o) v += t;
+    }
+    if (m < nr) s_num[m] = carry + v;
+    carry += __shfl(v, 63);
+  }
+  __syncthreads();
+  for (int m0 = 0; m0 < nr; m0 += 64) {
+    const int m = m0 + lane;
+    if (m < nr) {
+      const int key = s_num[m] + LINENUM_OFF;
+      if (key < 0 || key >= LINENUM_SPAN) {
+        s_flag = 1;
+      } else if (m == nr - 1 || s_num[m + 1] != s_num[m]) {
+        s_key[key] = (double)pk[s_ridx[m]];
+        s_has[key] = 1;
+        s_orig[key] = 1;
+      }
+    }
+  }
+  __syncthreads();
+  if (s_flag) {
+    if (lane == 0) R->status = FS_LINELOCS;
+    return;
+  }
+  // 5. fill missing line numbers 1..linecount+4: interpolation / head
+  //    extrapolation in parallel (they read original entries only)
+  for (int l = 1 + lane; l < linecount + 5; l += 64) {
     const int kl = l + LINENUM_OFF;
     if (s_orig[kl]) continue;
     int pv = -100000, nv = -100000;
     for (int q = l; q > -10; q--) if (s_orig[q + LINENUM_OFF]) { pv = q; break; }
     for (int q = l; q < linecount + 1; q++) if (s_orig[q + LINENUM_OFF]) { nv = q; break; }
+    if (nv == -100000) {
+      if (pv == -100000) s_flag = 1;    // linelocs[None] KeyError
+      continue;                         // tail: step 6
+    }
     double v;
     if (pv == -100000) {
-      if (nv == -100000) { R->status = FS_LINELOCS; return; }   // linelocs[None] KeyError
       v = s_key[nv + LINENUM_OFF] - (inl * (double)(nv - l));
-    } else if (nv != -100000) {
-      const double step = (s_key[nv + LINENUM_OFF] - s_key[pv + LINENUM_OFF]) / (double)(nv - pv);
-      v = s_key[pv + LINENUM_OFF] + (step * (double)(l - pv));
     } else {
-      const int kprev = pv - 1 + LINENUM_OFF;
-      if (!s_has[kprev]) { R->status = FS_LINELOCS; return; }   // linelocs2[prev_valid - 1] KeyError
-      const double step = s_key[pv + LINENUM_OFF] - s_key[kprev];
+      const double step = (s_key[nv + LINENUM_OFF] - s_key[pv + LINENUM_OFF]) / (double)(nv - pv);
       v = s_key[pv + LINENUM_OFF] + (step * (double)(l - pv));
     }
     s_key[kl] = v;
     s_has[kl] = 1;
   }
-  for (int l = 1; l < linecount + 5; l++) {
+  __syncthreads();
+  if (s_flag) {
+    if (lane == 0) R->status = FS_LINELOCS;
+    return;
+  }
+  // 6. tail extrapolation past the last valid line (uses earlier fills), in order
+  if (lane == 0) {
+    for (int l = 1; l < linecount + 5; l++) {
+      const int kl = l + LINENUM_OFF;
+      if (s_has[kl]) continue;
+      int pv = -100000;
+      for (int q = l; q > -10; q--) if (s_orig[q + LINENUM_OFF]) { pv = q; break; }
+      const int kprev = pv - 1 + LINENUM_OFF;
+      if (!s_has[kprev]) { s_flag = 1; break; }   // linelocs2[prev_valid - 1] KeyError
+      const double step = s_key[pv + LINENUM_OFF] - s_key[kprev];
+      s_key[kl] = s_key[pv + LINENUM_OFF] + (step * (double)(l - pv));
+      s_has[kl] = 1;
+    }
+  }
+  __syncthreads();
+  if (s_flag) {
+    if (lane == 0) R->status = FS_LINELOCS;
+    return;
+  }
+  double* L1 = lines + (int64_t)slot * LINES_STRIDE + LL1 * MAX_LINES;
+  int8_t* B1 = bad + (int64_t)slot * MAX_LINES;
+  for (int l = 1 + lane; l < linecount + 5; l += 64) {
     L1[l - 1] = s_key[l + LINENUM_OFF];
     B1[l - 1] = (l - 1 < 10) ? 0 : (s_orig[l + LINENUM_OFF] ? 0 : 1);
   }
 }
 
 // ---------------------------------------------------------------------------
-// refine_linelocs_hsync (lddecode_core.py:715-787).
-// grid: n_reads x 256 threads: per-line crossing searches in parallel, then
-// the sequential bad-line extrapolation and the two end fix-ups on thread 0.
-extern "C" __global__ __launch_bounds__(256) void ldg_k_hsync(
+// refine_linelocs_hsync (lddecode_core.py:715-787), part 1: the per-line
+// crossing search and bad-line tests, one wave per line.  Writes the line's
+// refined location to LL2 and its flag to bad[] (0 ok, 1 bad, 2 the reference
+// raises on this line).  grid: n_reads * MAX_LINES workgroups of 64 threads.
+extern "C" __global__ __launch_bounds__(64) void ldg_k_hsync_lines(
     const int32_t* __restrict__ smap, const double* __restrict__ video, int64_t vread_stride, int64_t vchan_stride, SysConst C,
     FieldRec* __restrict__ recs, double* __restrict__ lines, int8_t* __restrict__ bad) {
+  __shared__ double s_tmp[20];
+  const int lane = threadIdx.x;
+  const int slot = smap[blockIdx.x / MAX_LINES];
+  const int i = blockIdx.x % MAX_LINES;
+  FieldRec* R = recs + slot;
+  if (R->status != FS_PENDING) return;
+  if (i >= R->nlines) return;
+  const double* d05 = video + (int64_t)slot * vread_stride + (int64_t)CH_05 * vchan_stride;
+  const int64_t len = R->n_out;
+  const double* L1 = lines + (int64_t)slot * LINES_STRIDE + LL1 * MAX_LINES;
+  double* L2 = lines + (int64_t)slot * LINES_STRIDE + LL2 * MAX_LINES;
+  int8_t* B = bad + (int64_t)slot * MAX_LINES;
+  const double fr = C.freq;
+  auto hz = [&](double ire) { return C.ire0 + (C.hz_ire * ire); };
+  auto finish = [&](double v, int flag) {
+    if (lane == 0) { L2[i] = v; B[i] = (int8_t)flag; }
+  };
+  double v = L1[i];
+  bool lb = B[i] != 0;
+  if (i < 9) v -= 200;
+  const double ll1 = v;
+  double zc;
+  const int rc = wave_calczc(d05, len, v, hz(-20), 400, lane, &zc);
+  if (rc < 0) { finish(v, 2); return; }
+  if (rc == 0 && !lb) {
+    v = zc;
+    if (i >= 10) {
+      int64_t a1, b1, ah, bh, ab, bb;
+      py_slice(py_int(ll1 - (fr * 2)), py_int(ll1 + (fr * 2)), len, a1, b1);
+      py_slice(py_int(zc - (fr * 1)), py_int(zc + (fr * 3)), len, ah, bh);
+      py_slice(py_int(zc + (fr * 1)), py_int(zc + (fr * 3)), len, ab, bb);
+      // evaluation order of the reference's `or` chain; an empty window raises
+      bool isbad = false, raised = false;
+      auto grp = [&](int64_t a, int64_t b, double lo, double hi) -> bool {
+        if (a >= b) { raised = true; return true; }
+        if (wave_minmax_np(d05, a, b, false, lane) < lo) return true;
+        return wave_minmax_np(d05, a, b, true, lane) > hi;
+      };
+      if (grp(ah, bh, hz(-60), hz(20))) isbad = true;
+      else if (grp(a1, b1, hz(-60), hz(100))) isbad = true;
+      else if (grp(ab, bb, hz(-10), hz(10))) isbad = true;
+      if (raised) { finish(v, 2); return; }
+      if (isbad) {
+        lb = true;
+      } else {
+        const int64_t wl = bh - ah;
+        int64_t lo, hi;
+        py_slice(0, 20, wl, lo, hi);
+        if (lane < hi - lo) s_tmp[lane] = d05[ah + lo + lane];
+        __syncthreads();
+        const double low = np_mean(s_tmp, (int)(hi - lo));
+        __syncthreads();
+        py_slice(100, 120, wl, lo, hi);
+        if (lane < hi - lo) s_tmp[lane] = d05[ah + lo + lane];
+        __syncthreads();
+        const double high = np_mean(s_tmp, (int)(hi - lo));
+        double zc2;
+        const int rc2 = wave_calczc(d05 + ah, wl, 0, (low + high) / 2, wl, lane, &zc2);
+        if (rc2 != 0) { finish(v, 2); return; }   // None += ... -> TypeError
+        zc2 += ((double)py_int(zc) - (fr * 1));
+        if (fabs(zc2 - zc) < (fr / 4)) v = zc2;
+        else lb = true;
+      }
+    }
+  } else {
+    lb = true;
+  }
+  finish(v, lb ? 1 : 0);
+}
+
+// refine_linelocs_hsync, part 2 (per read): bad-line extrapolation and the
+// two end fix-ups, sequential as in the reference, in LDS on thread 0.
+extern "C" __global__ __launch_bounds__(256) void ldg_k_hsync_field(const int32_t* __restrict__ smap, SysConst C,
+                                                                   FieldRec* __restrict__ recs,
+                                                                   double* __restrict__ lines,
+                                                                   int8_t* __restrict__ bad) {
   __shared__ double s_v[MAX_LINES];
   __shared__ int8_t s_bad[MAX_LINES];
   __shared__ int s_err;
@@ -503,91 +665,44 @@ extern "C" __global__ __launch_bounds__(256) void ldg_k_hsync(
   FieldRec* R = recs + slot;
   if (R->status != FS_PENDING) return;
   const int nl = R->nlines;
-  const double* d05 = video + (int64_t)slot * vread_stride + (int64_t)CH_05 * vchan_stride;
-  const int64_t len = R->n_out;
-  const double* L1 = lines + (int64_t)slot * LINES_STRIDE + LL1 * MAX_LINES;
   double* L2 = lines + (int64_t)slot * LINES_STRIDE + LL2 * MAX_LINES;
   int8_t* B = bad + (int64_t)slot * MAX_LINES;
-  const double fr = C.freq;
-  auto hz = [&](double ire) { return C.ire0 + (C.hz_ire * ire); };
   if (tid == 0) s_err = 0;
   __syncthreads();
   for (int i = tid; i < nl; i += 256) {
-    double v = L1[i];
-    bool lb = B[i] != 0;
-    if (i < 9) v -= 200;
-    const double ll1 = v;
-    double zc;
-    const int rc = calczc(d05, len, v, hz(-20), 400, &zc);
-    if (rc < 0) { atomicOr(&s_err, 1); continue; }
-    if (rc == 0 && !lb) {
-      v = zc;
-      if (i >= 10) {
-        int64_t a1, b1, ah, bh, ab, bb;
-        py_slice(py_int(ll1 - (fr * 2)), py_int(ll1 + (fr * 2)), len, a1, b1);
-        py_slice(py_int(zc - (fr * 1)), py_int(zc + (fr * 3)), len, ah, bh);
-        py_slice(py_int(zc + (fr * 1)), py_int(zc + (fr * 3)), len, ab, bb);
-        auto mn = [&](int64_t a, int64_t b) { double m = d05[a]; for (int64_t k = a + 1; k < b; k++) m = fmin(m, d05[k]); return m; };
-        auto mx = [&](int64_t a, int64_t b) { double m = d05[a]; for (int64_t k = a + 1; k < b; k++) m = fmax(m, d05[k]); return m; };
-        // evaluation order of the reference's `or` chain; an empty window raises
-        bool isbad = false, raised = false;
-        auto grp = [&](int64_t a, int64_t b, double lo, double hi) -> bool {
-          if (a >= b) { raised = true; return true; }
-          if (mn(a, b) < lo) return true;
-          return mx(a, b) > hi;
-        };
-        if (grp(ah, bh, hz(-60), hz(20))) isbad = true;
-        else if (grp(a1, b1, hz(-60), hz(100))) isbad = true;
-        else if (grp(ab, bb, hz(-10), hz(10))) isbad = true;
-        if (raised) { atomicOr(&s_err, 1); continue; }
-        if (isbad) {
-          lb = true;
-        } else {
-          const int64_t wl = bh - ah;
-          double tmp[20];
-          int64_t lo, hi;
-          py_slice(0, 20, wl, lo, hi);
-          for (int64_t k = lo; k < hi; k++) tmp[k - lo] = d05[ah + k];
-          const double low = np_mean(tmp, (int)(hi - lo));
-          py_slice(100, 120, wl, lo, hi);
-          for (int64_t k = lo; k < hi; k++) tmp[k - lo] = d05[ah + k];
-          const double high = np_mean(tmp, (int)(hi - lo));
-          double zc2;
-          const int rc2 = calczc(d05 + ah, wl, 0, (low + high) / 2, wl, &zc2);
-          if (rc2 != 0) { atomicOr(&s_err, 1); continue; }   // None += ... -> TypeError
-          zc2 += ((double)py_int(zc) - (fr * 1));
-          if (fabs(zc2 - zc) < (fr / 4)) v = zc2;
-          else lb = true;
-        }
-      }
-    } else {
-      lb = true;
-    }
-    s_v[i] = v;
-    s_bad[i] = lb ? 1 : 0;
+    s_v[i] = L2[i];
+    const int8_t f = B[i];
+    s_bad[i] = f;
+    if (f == 2) atomicOr(&s_err, 1);
   }
   __syncthreads();
-  if (tid != 0) return;
-  if (s_err) { R->status = FS_LINELOCS; return; }
-  for (int i = 0; i < nl; i++) {
-    if (i < 10) s_v[i] += 4.72 * fr;
-    if (i > 10 && s_bad[i]) {
-      const double gap = s_v[i - 1] - s_v[i - 2];
+  if (s_err) {
+    if (tid == 0) R->status = FS_LINELOCS;
+    return;
+  }
+  const double fr = C.freq;
+  if (tid == 0) {
+    for (int i = 0; i < nl; i++) {
+      if (i < 10) s_v[i] += 4.72 * fr;
+      if (i > 10 && s_bad[i]) {
+        const double gap = s_v[i - 1] - s_v[i - 2];
+        s_v[i] = s_v[i - 1] + gap;
+      }
+    }
+    const double lo = C.linelen - (fr * .2), hi = C.linelen + (fr * .2);
+    for (int i = 9; i >= 0; i--) {
+      double gap = s_v[i + 1] - s_v[i];
+      if (!inrange(gap, lo, hi)) gap = C.linelen;
+      s_v[i] = s_v[i + 1] - gap;
+    }
+    for (int i = nl - 10; i < nl; i++) {
+      double gap = s_v[i] - s_v[i - 1];
+      if (!inrange(gap, lo, hi)) gap = C.linelen;
       s_v[i] = s_v[i - 1] + gap;
     }
   }
-  const double lo = C.linelen - (fr * .2), hi = C.linelen + (fr * .2);
-  for (int i = 9; i >= 0; i--) {
-    double gap = s_v[i + 1] - s_v[i];
-    if (!inrange(gap, lo, hi)) gap = C.linelen;
-    s_v[i] = s_v[i + 1] - gap;
-  }
-  for (int i = nl - 10; i < nl; i++) {
-    double gap = s_v[i] - s_v[i - 1];
-    if (!inrange(gap, lo, hi)) gap = C.linelen;
-    s_v[i] = s_v[i - 1] + gap;
-  }
-  for (int i = 0; i < nl; i++) { L2[i] = s_v[i]; B[i] = s_bad[i]; }
+  __syncthreads();
+  for (int i = tid; i < nl; i += 256) { L2[i] = s_v[i]; B[i] = s_bad[i]; }
 }
 
 // ---------------------------------------------------------------------------

@@ -94,6 +94,58 @@ __device__ inline int calczc(const double* data, int64_t len, double start_offse
   return 0;
 }
 
+// ---- one-wave (64 lanes, all calling) versions of the scans above ----------
+// first k in [lo, hi) with data[k] >= target (rising) / <= target, or -1
+__device__ inline int64_t wave_find_first(const double* data, int64_t lo, int64_t hi, bool rising, double target,
+                                          int lane) {
+  for (int64_t k0 = lo; k0 < hi; k0 += 64) {
+    const int64_t k = k0 + lane;
+    bool p = false;
+    if (k < hi) { const double v = data[k]; p = rising ? (v >= target) : (v <= target); }
+    const uint64_t m = __ballot(p);
+    if (m) return k0 + (__ffsll((unsigned long long)m) - 1);
+  }
+  return -1;
+}
+
+// calczc above, wave-parallel search (same result and error semantics)
+__device__ inline int wave_calczc(const double* data, int64_t len, double start_offset, double target, int64_t count,
+                                  int lane, double* res) {
+  const int64_t s = py_int(start_offset);
+  const int64_t n = count + 1;
+  int64_t si;
+  if (!py_index(s, len, si)) return -1;
+  const bool rising = data[si] < target;
+  int64_t lo, hi;
+  py_slice(s, s + n, len, lo, hi);
+  const int64_t k = wave_find_first(data, lo, hi, rising, target, lane);
+  if (k < 0) return 1;
+  const int64_t x = s + (k - lo);
+  if (x == 0) return 1;
+  int64_t ia, ib;
+  if (!py_index(x - 1, len, ia) || !py_index(x, len, ib)) return -1;
+  const double a = data[ia] - target;
+  const double b = data[ib] - target;
+  *res = (double)(x - 1) + ((-a) / ((-a) + b));
+  return 0;
+}
+
+// np.min / np.max of data[a, b) (b > a): NaN if any element is NaN
+__device__ inline double wave_minmax_np(const double* data, int64_t a, int64_t b, bool is_max, int lane) {
+  double m = is_max ? -__builtin_inf() : __builtin_inf();
+  bool nan = false;
+  for (int64_t k = a + lane; k < b; k += 64) {
+    const double v = data[k];
+    if (v != v) nan = true;
+    else m = is_max ? fmax(m, v) : fmin(m, v);
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    const double t = __shfl_xor(m, o);
+    m = is_max ? fmax(m, t) : fmin(m, t);
+  }
+  return __ballot(nan) ? __builtin_nan("") : m;
+}
+
 // Sorted-window median helper: median of a[0..n) already sorted ascending.
 __device__ inline double sorted_median(const double* a, int n) {
   if (n <= 0) return __builtin_nan("");

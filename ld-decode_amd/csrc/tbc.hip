@@ -7,12 +7,11 @@
 // (:1023-1035), downscale_audio (:431-484) and Framer.formatoutput (:1238-1252).
 //
 // Spline: scipy splrep(s=0) on unit-spaced points is the not-a-knot cubic
-// interpolant, solved in second-derivative form.  The burst pass (40 outputs
-// per line) runs one lane per line with a Thomas sweep over a window of rows
-// reaching KTR=40 samples past its outputs (exact to rho^40 ~ 1e-23 relative,
-// below double rounding; lane-interleaved scratch dp[t*64 + lane], coalesced).
-// The final pass runs one wave per line with the line in LDS and the
-// tridiagonal solve as chunked affine scans (spline_line_wave).
+// interpolant, solved in second-derivative form by one workgroup per line
+// (spline_block): the line's samples in LDS, the tridiagonal solve as chunked
+// affine scans.  The final pass solves the whole line on 256 threads; the
+// burst pass (40 outputs per line) solves only the rows within KTR=40 samples
+// of its outputs (exact to rho^40 ~ 1e-23 relative) on one wave.
 #include <hip/hip_runtime.h>
 #include "common.hpp"
 #include "field_rec.hpp"
@@ -35,201 +34,157 @@ constexpr CTab make_ctab() {
 __constant__ CTab g_ctab = make_ctab();        // Thomas c'_t for diag 4 / off-diag 1 (fixed point from t=14)
 __device__ __forceinline__ double ctab(int64_t t) { return g_ctab.v[t < 16 ? t : 16]; }
 
-// Truncation margin of the windowed spline solve: the interior system
-// (1,4,1) couples M_j to its neighbours with decay rho = 2 - sqrt(3) per
-// sample, so cutting the system KTR rows beyond the needed range perturbs
-// the result by < rho^KTR ~ 1.5e-23 (relative) -- below double rounding.
+// Truncation margin of a windowed spline solve (the burst pass needs 40 of a
+// line's outputs): the interior system (1,4,1) couples M_j to its neighbours
+// with decay rho = 2 - sqrt(3) per sample, so cutting the system KTR rows
+// beyond the needed range perturbs the result by < rho^KTR ~ 1.5e-23
+// (relative) -- below double rounding.
 constexpr int KTR = 40;
-constexpr int SCR_LANE = 512;                 // Thomas scratch entries per lane
-constexpr int64_t SCR_PER_SLOT = (int64_t)LINE_GROUPS * 64 * SCR_LANE;   // burst pass
+constexpr int64_t SCR_PER_SLOT = (int64_t)MAX_LINES * 64 + 3 * MAX_LINES;   // PAL pilot offsets (PILOT_MAX = 64) per slot
 
 // Not-a-knot cubic spline through y[j] = buf[ib + j], j = 0..n (lddutils.scale:
 // splrep(s=0) on unit spacing), evaluated at x_o = o*step + x0 (numpy
-// linspace(begin-ib, end-ib, W+1) arithmetic) for o in [o_lo, o_hi), visiting o
-// in descending order: sink(o, value).
-//
-// Second-derivative form.  The not-a-knot rows fold into M_1 = r_1/6 and
-// M_{n-1} = r_{n-1}/6; rows 2..n-2 are tridiagonal (1,4,1).  Only the rows
-// [jlo-KTR, jhi+1+KTR] around the intervals the requested outputs fall in are
-// solved (exact boundary values where the window reaches a line end), so a
-// line can be split over several lanes.  dp: this lane's scratch, entry t at
-// dp[t * ST].  Returns 0, or -1 where splrep would raise.
-template <int ST, class Sink>
-__device__ int spline_window(const double* __restrict__ buf, int64_t len, double begin, double end, int W, int o_lo,
-                             int o_hi, double* __restrict__ dp, Sink&& sink) {
+// linspace(begin-ib, end-ib, W+1) arithmetic).  Second-derivative form: the
+// not-a-knot rows fold into M_1 = r_1/6 and M_{n-1} = r_{n-1}/6; rows 2..n-2
+// are tridiagonal (1,4,1) with right-hand side r_j = 6 (y_{j+1} - 2 y_j + y_{j-1});
+// M_0 = 2 M_1 - M_2, M_n = 2 M_{n-1} - M_{n-2}.
+// spline_block: the interpolant on one workgroup of NT threads (NT = 64 * waves).
+// Rows [lo, hi] around the requested outputs (the whole line for the final
+// pass; KTR rows past the outputs otherwise, exactly as spline_window) are
+// solved with the line's samples staged in LDS (one coalesced load) and the
+// tridiagonal solve as chunked affine scans: thread i owns rows
+// [i*CH, (i+1)*CH) (CH odd: conflict-free strided LDS access), composes its
+// rows' maps, a workgroup Kogge-Stone scan gives each chunk its carry-in, and
+// the thread re-runs its rows with the Thomas arithmetic (forward d_t = (r_t -
+// d_{t-1}) c_t, backward M_t = d_t - c_t M_{t+1}) into ms.  Outputs
+// o = o_lo + tid + NT q < o_hi: sink(o, value).  Returns -1 (uniform) where
+// splrep would raise.
+template <int NT, int CAP = SPL_MAXN + 1>
+struct SplineLDS {
+  static constexpr int cap = CAP;   // samples [base, top] of the solved window
+  double ys[CAP];
+  double ms[CAP];
+  double ct[17];
+  double wa[NT / 64], wb[NT / 64];
+  double carry[NT];
+  double m1, mn1;
+};
+
+// Inclusive scan of affine maps x -> A x + B over the workgroup's threads in
+// order (suffix: in reverse order); returns the carry-in of this thread's
+// chunk, i.e. the composition of all earlier (later) chunks applied to 0.
+template <int NT, class SL>
+__device__ __forceinline__ double block_affine_carry(double A, double B, bool suffix, int tid, SL& S) {
+  const int lane = tid & 63, wv = tid >> 6;
+  constexpr int NW = NT / 64;
+  for (int o = 1; o < 64; o <<= 1) {
+    const double pa = suffix ? __shfl_down(A, o) : __shfl_up(A, o);
+    const double pb = suffix ? __shfl_down(B, o) : __shfl_up(B, o);
+    if (suffix ? (lane + o < 64) : (lane >= o)) { B = A * pb + B; A = A * pa; }
+  }
+  if constexpr (NW > 1) {
+    if (lane == (suffix ? 0 : 63)) { S.wa[wv] = A; S.wb[wv] = B; }
+    __syncthreads();
+    if (suffix) {
+      for (int w = wv + 1; w < NW; w++) { B = A * S.wb[w] + B; A = A * S.wa[w]; }
+    } else {
+      for (int w = wv - 1; w >= 0; w--) { B = A * S.wb[w] + B; A = A * S.wa[w]; }
+    }
+  }
+  S.carry[tid] = B;
+  __syncthreads();
+  const double c = suffix ? (tid + 1 < NT ? S.carry[tid + 1] : 0.0) : (tid ? S.carry[tid - 1] : 0.0);
+  __syncthreads();
+  return c;
+}
+
+template <int NT, class SL, class Sink>
+__device__ int spline_block(const double* __restrict__ buf, int64_t len, double begin, double end, int W, int o_lo,
+                            int o_hi, int tid, SL& S, Sink&& sink) {
+  if (tid < 17) S.ct[tid] = g_ctab.v[tid];
   const int64_t ib = py_int(begin), ie = py_int(end);
-  const int64_t n = ie - ib;
-  if (ib < 0 || n < 6 || n >= SPL_MAXN || ib + n + 1 > len) return -1;
+  const int64_t n64 = ie - ib;
+  if (ib < 0 || n64 < 6 || n64 >= SPL_MAXN || ib + n64 + 1 > len) return -1;
+  const int n = (int)n64;
   const double* y = buf + ib;
-  auto rr = [&](int64_t j) { return 6.0 * ((y[j + 1] - y[j]) - (y[j] - y[j - 1])); };
-  const double M1 = rr(1) / 6.0, Mn1 = rr(n - 1) / 6.0;
   const double x0 = begin - (double)ib;
   const double span = end - begin;
   const double step = ((span + x0) - x0) / (double)W;
   auto xo = [&](int o) { double x = (double)o * step; return x + x0; };
   auto ival = [&](double x) {
     int64_t j = (int64_t)floor(x);
-    return j < 0 ? (int64_t)0 : (j > n - 1 ? n - 1 : j);
+    return (int)(j < 0 ? 0 : (j > n - 1 ? n - 1 : j));
   };
-  const int64_t jlo = ival(xo(o_lo)), jhi = ival(xo(o_hi - 1));
-  const int64_t lo = (jlo - KTR > 2) ? jlo - KTR : 2;
-  const int64_t hi = (jhi + 1 + KTR < n - 2) ? jhi + 1 + KTR : n - 2;
-  const int64_t N = hi - lo + 1;
-  if (N > SCR_LANE) return -1;
-  const double BL = (lo == 2) ? M1 : 0.0, BR = (hi == n - 2) ? Mn1 : 0.0;
-  double dprev = 0.0;
-  for (int64_t t = 0; t < N; t++) {
-    double rhs = rr(lo + t);
-    if (t == 0) rhs -= BL;
-    if (t == N - 1) rhs -= BR;
-    const double d = (rhs - dprev) * ctab(t);
-    dp[t * ST] = d;
-    dprev = d;
+  const int jlo = ival(xo(o_lo)), jhi = ival(xo(o_hi - 1));
+  const int lo = (jlo - KTR > 2) ? jlo - KTR : 2;
+  const int hi = (jhi + 1 + KTR < n - 2) ? jhi + 1 + KTR : n - 2;
+  const int base = (lo - 1 < jlo) ? lo - 1 : jlo;            // ys / ms hold j in [base, top]
+  const int top = (hi + 1 > jhi + 1) ? hi + 1 : jhi + 1;
+  if (top - base + 1 > SL::cap) return -1;                    // unreachable for n < SPL_MAXN (see callers)
+  double* ys = S.ys - base;
+  double* ms = S.ms - base;
+  for (int j = base + tid; j <= top; j += NT) ys[j] = y[j];
+  if (tid == 0) {
+    S.m1 = (6.0 * ((y[2] - y[1]) - (y[1] - y[0]))) / 6.0;
+    S.mn1 = (6.0 * ((y[n] - y[n - 1]) - (y[n - 1] - y[n - 2]))) / 6.0;
   }
-  int o = o_hi - 1;
-  auto emit = [&](int64_t k, double Mk, double Mk1, bool lowest) {
-    const double yk = y[k], yk1 = y[k + 1];
-    while (o >= o_lo) {
-      const double x = xo(o);
-      if (!lowest && x < (double)k) break;
-      const double a = (double)(k + 1) - x, b = x - (double)k;
-      const double v = Mk * a * a * a / 6.0 + Mk1 * b * b * b / 6.0 + (yk - Mk / 6.0) * a + (yk1 - Mk1 / 6.0) * b;
-      sink(o, v);
-      o--;
-    }
-  };
-  const double Mhi = dp[(N - 1) * ST];
-  double Mnext = 0.0;                        // M_{k+1}
-  if (hi == n - 2) {
-    // interval n-1: (M_{n-1}, M_n = 2 M_{n-1} - M_{n-2}) -- the not-a-knot end piece
-    if (jhi == n - 1) emit(n - 1, Mn1, 2.0 * Mn1 - Mhi, jlo == n - 1);
-    Mnext = Mn1;
-  }
-  const int64_t kstop = jlo > lo ? jlo : lo;
-  for (int64_t k = hi; k >= kstop && o >= o_lo; k--) {
-    const int64_t t = k - lo;
-    const double Mk = (t == N - 1) ? Mhi : dp[t * ST] - ctab(t) * Mnext;
-    if (k <= jhi) emit(k, Mk, Mnext, k == jlo);
-    Mnext = Mk;
-  }
-  if (o >= o_lo && jlo < lo) {               // lo == 2: the not-a-knot start piece
-    const double M2 = Mnext;
-    if (jhi >= 1) emit(1, M1, M2, jlo == 1);
-    if (o >= o_lo) emit(0, 2.0 * M1 - M2, M1, true);
-  }
-  return 0;
-}
-
-// The same interpolant for a whole line on one wave, outputs o = lane + 64 q.
-// The line's samples go to LDS (ys) with one coalesced load; the tridiagonal
-// solve for M_2..M_{n-2} runs as chunked affine scans: lane l owns rows
-// [l*CH, (l+1)*CH) (CH odd: conflict-free strided LDS access), composes its
-// rows' maps, a 64-lane Kogge-Stone scan yields each chunk's carry-in, and the
-// lane re-runs its rows with the Thomas arithmetic (forward d_t = (r_t -
-// d_{t-1}) c_t, backward M_t = d_t - c_t M_{t+1}) into ms.  Returns -1 (wave
-// uniform) where splrep would raise.
-template <class Sink>
-__device__ int spline_line_wave(const double* __restrict__ buf, int64_t len, double begin, double end, int W, int lane,
-                                double* __restrict__ ys, double* __restrict__ ms, double* __restrict__ ct, Sink&& sink) {
-  // c'_t table in LDS: the row index differs per lane, and a per-lane index
-  // into __constant__ memory is a vector memory load on the recurrence path
-  if (lane < 17) ct[lane] = g_ctab.v[lane];
-  auto ctab = [&](int t) { return ct[t < 16 ? t : 16]; };
-  const int64_t ib = py_int(begin), ie = py_int(end);
-  const int64_t n64 = ie - ib;
-  if (ib < 0 || n64 < 6 || n64 >= SPL_MAXN || ib + n64 + 1 > len) return -1;
-  const int n = (int)n64;
-  const double* y = buf + ib;
-  for (int j = lane; j <= n; j += 64) ys[j] = y[j];
   __syncthreads();
-  auto rr = [&](int j) { return 6.0 * ((ys[j + 1] - ys[j]) - (ys[j] - ys[j - 1])); };
-  const double M1 = rr(1) / 6.0, Mn1 = rr(n - 1) / 6.0;
-  const int T = n - 3;                                // rows j = t + 2, t in [0, T)
-  int CH = (T + 63) / 64;
+  const double M1 = S.m1, Mn1 = S.mn1;
+  const double BL = (lo == 2) ? M1 : 0.0, BR = (hi == n - 2) ? Mn1 : 0.0;
+  const int T = hi - lo + 1;                                  // rows j = lo + t
+  int CH = (T + NT - 1) / NT;
   CH |= 1;
-  const int t0 = lane * CH;
+  const int t0 = tid * CH;
   const int t1 = (t0 + CH < T) ? t0 + CH : T;
+  auto ct = [&](int t) { return S.ct[t < 16 ? t : 16]; };
   auto rhs = [&](int t) {
-    double r = rr(t + 2);
-    if (t == 0) r -= M1;
-    if (t == T - 1) r -= Mn1;
+    const int j = lo + t;
+    double r = 6.0 * ((ys[j + 1] - ys[j]) - (ys[j] - ys[j - 1]));
+    if (t == 0) r -= BL;
+    if (t == T - 1) r -= BR;
     return r;
   };
-  // forward: compose d -> -c d + c r over my rows
+  // forward sweep: d -> -c d + c r
   double A = 1.0, B = 0.0;
   for (int t = t0; t < t1; t++) {
-    const double c = ctab(t);
+    const double c = ct(t);
     A = -c * A;
     B = (rhs(t) - B) * c;
   }
-  for (int o = 1; o < 64; o <<= 1) {                   // inclusive scan of (A, B) over lanes
-    const double pa = __shfl_up(A, o), pb = __shfl_up(B, o);
-    if (lane >= o) { B = A * pb + B; A = A * pa; }
-  }
-  double dprev = __shfl_up(B, 1);
-  if (lane == 0) dprev = 0.0;
+  double dprev = block_affine_carry<NT>(A, B, false, tid, S);
   for (int t = t0; t < t1; t++) {
-    const double d = (rhs(t) - dprev) * ctab(t);
-    ms[t + 2] = d;
+    const double d = (rhs(t) - dprev) * ct(t);
+    ms[lo + t] = d;
     dprev = d;
   }
-  // backward: compose M -> d - c M over my rows, top down
+  // back substitution: M -> d - c M, top down
   A = 1.0; B = 0.0;
   for (int t = t1 - 1; t >= t0; t--) {
-    const double c = ctab(t);
+    const double c = ct(t);
     A = -c * A;
-    B = ms[t + 2] - c * B;
+    B = ms[lo + t] - c * B;
   }
-  for (int o = 1; o < 64; o <<= 1) {                   // inclusive suffix scan over lanes
-    const double pa = __shfl_down(A, o), pb = __shfl_down(B, o);
-    if (lane + o < 64) { B = A * pb + B; A = A * pa; }
-  }
-  double Mnext = __shfl_down(B, 1);
-  if (lane == 63) Mnext = 0.0;
+  double Mnext = block_affine_carry<NT>(A, B, true, tid, S);
   for (int t = t1 - 1; t >= t0; t--) {
-    const double M = ms[t + 2] - ctab(t) * Mnext;
-    ms[t + 2] = M;
+    const double M = ms[lo + t] - ct(t) * Mnext;
+    ms[lo + t] = M;
     Mnext = M;
   }
   __syncthreads();
-  if (lane == 0) {
-    ms[1] = M1;
-    ms[0] = 2.0 * M1 - ms[2];
-    ms[n - 1] = Mn1;
-    ms[n] = 2.0 * Mn1 - ms[n - 2];
+  if (tid == 0) {
+    if (lo == 2) { ms[1] = M1; if (base == 0) ms[0] = 2.0 * M1 - ms[2]; }
+    if (hi == n - 2) { ms[n - 1] = Mn1; if (top == n) ms[n] = 2.0 * Mn1 - ms[n - 2]; }
   }
   __syncthreads();
-  const double x0 = begin - (double)ib;
-  const double span = end - begin;
-  const double step = ((span + x0) - x0) / (double)W;
-  for (int o = lane; o < W; o += 64) {
-    double x = (double)o * step;
-    x = x + x0;
-    int64_t k = (int64_t)floor(x);
-    k = k < 0 ? 0 : (k > n - 1 ? n - 1 : k);
+  for (int o = o_lo + tid; o < o_hi; o += NT) {
+    const double x = xo(o);
+    const int k = ival(x);
     const double Mk = ms[k], Mk1 = ms[k + 1], yk = ys[k], yk1 = ys[k + 1];
     const double a = (double)(k + 1) - x, b = x - (double)k;
     const double v = Mk * a * a * a / 6.0 + Mk1 * b * b * b / 6.0 + (yk - Mk / 6.0) * a + (yk1 - Mk1 / 6.0) * b;
     sink(o, v);
   }
   return 0;
-}
-
-// strided numpy pairwise sum (same order as pw_sum over a[0], a[st], ...)
-__device__ inline double pwb_s(const double* a, int n, int st) {
-  if (n < 8) {
-    double r = -0.0;
-    for (int i = 0; i < n; i++) r += a[i * st];
-    return r;
-  }
-  double r[8];
-  for (int j = 0; j < 8; j++) r[j] = a[j * st];
-  int i = 8;
-  for (; i < n - (n % 8); i += 8)
-    for (int j = 0; j < 8; j++) r[j] += a[(i + j) * st];
-  double res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
-  for (; i < n; i++) res += a[i * st];
-  return 0.0 + res;
 }
 
 __device__ inline int calczc_s(const double* d, int len, int s, double target, int count, int st, double* res) {
@@ -257,16 +212,15 @@ __device__ inline int calczc_s(const double* d, int len, int s, double target, i
 // grid: n_reads * LINE_GROUPS workgroups of 64 threads; lane = line.
 extern "C" __global__ __launch_bounds__(64) void ldg_k_burst_lines(
     const int32_t* __restrict__ smap, const double* __restrict__ video, int64_t vread_stride, int64_t vchan_stride, SysConst C,
-    FieldRec* __restrict__ recs, double* __restrict__ lines, float* __restrict__ blevel,
-    double* __restrict__ scratch, int pass) {
-  __shared__ double s_ba[40 * 64];
-  __shared__ double s_t[40 * 64];
+    FieldRec* __restrict__ recs, double* __restrict__ lines, float* __restrict__ blevel, int pass) {
+  // window rows for 40 outputs: <= 40 * SPL_MAXN / W + 2 * KTR + 4 < 384
+  __shared__ SplineLDS<64, 384> S;
+  __shared__ double s_ba[40], s_t[40], s_g[2][40];
   const int lane = threadIdx.x;
-  const int slot = smap[blockIdx.x / LINE_GROUPS];
-  const int grp = blockIdx.x % LINE_GROUPS;
+  const int slot = smap[blockIdx.x / MAX_LINES];
+  const int l = blockIdx.x % MAX_LINES;
   FieldRec* R = recs + slot;
   if (R->status != FS_PENDING) return;
-  const int l = grp * 64 + lane;
   const int nl = R->nlines, lc = R->linecount;
   double* LN = lines + (int64_t)slot * LINES_STRIDE;
   const double* li = LN + (pass == 0 ? LL2 : LL3) * MAX_LINES;
@@ -274,28 +228,34 @@ extern "C" __global__ __launch_bounds__(64) void ldg_k_burst_lines(
   double* pv1 = LN + PAVG1 * MAX_LINES;
   float* lvl = blevel + (int64_t)slot * MAX_LINES;
   if (l >= nl) return;
-  if (l >= lc) { pv0[l] = 0.0; pv1[l] = 0.0; lvl[l] = 0.0f; return; }
+  if (l >= lc) {
+    if (lane == 0) { pv0[l] = 0.0; pv1[l] = 0.0; lvl[l] = 0.0f; }
+    return;
+  }
   const double* bur = video + (int64_t)slot * vread_stride + (int64_t)CH_BURST * vchan_stride;
-  double* dp = scratch + (int64_t)slot * SCR_PER_SLOT + (int64_t)grp * 64 * SCR_LANE + lane;
-  double* ba = s_ba + lane;
-  double* tt = s_t + lane;
   const double b0 = li[l], b1 = li[l + 1];
   const double wow = (b1 - b0) / (double)C.linelen;
   const int W = C.outlinelen;
-  const int rc = spline_window<64>(bur, R->n_out, b0, b1, W, 20, 60, dp,
-                                   [&](int o, double v) { ba[(o - 20) * 64] = v * wow; });
-  if (rc < 0) { R->status = FS_TBC; return; }   // benign race: every writer stores the same value
-
+  const int rc = spline_block<64>(bur, R->n_out, b0, b1, W, 20, 60, lane, S,
+                                  [&](int o, double v) { s_ba[o - 20] = v * wow; });
+  if (rc < 0) {
+    if (lane == 0) R->status = FS_TBC;   // benign race: every writer stores the same value
+    return;
+  }
+  __syncthreads();
+  if (lane != 0) return;
+  double* ba = s_ba;
+  double* tt = s_t;
   const double hzs = 1700000 / 140.0;
-  const double m = pwb_s(ba, 40, 64) / 40.0;
+  const double m = pw_sum(ba, 40) / 40.0;
   double mx = 0.0;
-  for (int i = 0; i < 40; i++) { const double v = ba[i * 64] - m; ba[i * 64] = v; mx = fmax(mx, fabs(v)); }
+  for (int i = 0; i < 40; i++) { const double v = ba[i] - m; ba[i] = v; mx = fmax(mx, fabs(v)); }
   const float lf = (float)mx;
   const double lv = (double)lf;               // numpy-1: float32 element promoted to float64
   // np.std(ba)
-  const double m2 = pwb_s(ba, 40, 64) / 40.0;
-  for (int i = 0; i < 40; i++) { const double d = ba[i * 64] - m2; tt[i * 64] = d * d; }
-  const double sd = sqrt(pwb_s(tt, 40, 64) / 40.0);
+  const double m2 = pw_sum(ba, 40) / 40.0;
+  for (int i = 0; i < 40; i++) { const double d = ba[i] - m2; tt[i] = d * d; }
+  const double sd = sqrt(pw_sum(tt, 40) / 40.0);
   double p0 = 0.0, p1 = 0.0;
   float out_level = lf;
   if (((lv / hzs) > 30) || (sd / hzs) < 3) {
@@ -306,13 +266,13 @@ extern "C" __global__ __launch_bounds__(64) void ldg_k_burst_lines(
     int cnt = 0, nF = 0, nT = 0;
     int bi = 0;
     while (bi < 40) {
-      if (fabs(ba[bi * 64]) > lv * .6) {
+      if (fabs(ba[bi]) > lv * .6) {
         double zc;
-        if (calczc_s(ba, 40, bi, 0.0, 10, 64, &zc) == 0) {
+        if (calczc_s(ba, 40, bi, 0.0, 10, 1, &zc) == 0) {
           double off = zc - ((floor(zc / 4) * 4) - 1);
           if (off > 3.5) off -= 4;
-          const bool pos = ba[bi * 64] > 0;
-          tt[cnt * 64] = off;
+          const bool pos = ba[bi] > 0;
+          tt[cnt] = off;
           if (pos) { tag |= (1ull << cnt); nT++; } else nF++;
           cnt++;
           bi = (int)zc;
@@ -322,11 +282,12 @@ extern "C" __global__ __launch_bounds__(64) void ldg_k_burst_lines(
     }
     if (!(nF < 3 || nT < 3)) {
       // mean of each group's [1:-1] (np.array of the list, pairwise sum)
-      double gF[40], gT[40];
+      double* gF = s_g[0];
+      double* gT = s_g[1];
       int kF = 0, kT = 0;
       for (int k = 0; k < cnt; k++) {
-        if ((tag >> k) & 1) gT[kT++] = tt[k * 64];
-        else gF[kF++] = tt[k * 64];
+        if ((tag >> k) & 1) gT[kT++] = tt[k];
+        else gF[kF++] = tt[k];
       }
       const double mF = pw_sum(gF + 1, kF - 2) / (double)(kF - 2);
       const double mT = pw_sum(gT + 1, kT - 2) / (double)(kT - 2);
@@ -407,14 +368,13 @@ extern "C" __global__ __launch_bounds__(64) void ldg_k_burst_field(const int32_t
 // Final resample of 'demod' (lineoffset 1 NTSC / 3 PAL, wow) to uint16 .tbc
 // lines (lddecode_core.py:1135-1159 NTSC, :1023-1035 PAL).
 // grid: n_reads * LINE_GROUPS workgroups of 64 threads; lane = output row.
-extern "C" __global__ __launch_bounds__(64) void ldg_k_final_lines(
+constexpr int FINAL_NT = 256;
+extern "C" __global__ __launch_bounds__(FINAL_NT) void ldg_k_final_lines(
     const int32_t* __restrict__ smap, const double* __restrict__ video, int64_t vread_stride, int64_t vchan_stride,
     SysConst C, FieldRec* __restrict__ recs, const double* __restrict__ lines, const float* __restrict__ blevel,
     uint16_t* __restrict__ pic, int64_t pic_stride) {
-  __shared__ double s_y[SPL_MAXN + 1];
-  __shared__ double s_m[SPL_MAXN + 1];
-  __shared__ double s_ct[17];
-  const int lane = threadIdx.x;
+  __shared__ SplineLDS<FINAL_NT> S;
+  const int tid = threadIdx.x;
   const int slot = smap[blockIdx.x / MAX_LINES];
   const int row = blockIdx.x % MAX_LINES;
   FieldRec* R = recs + slot;
@@ -433,7 +393,7 @@ extern "C" __global__ __launch_bounds__(64) void ldg_k_final_lines(
   const double scale_ = pal ? (double)(0xd300 - 0x0100) / (100 - C.vsync_ire)
                             : (double)(0xc800 - 0x0400) / (100 - C.vsync_ire);
   const double base = pal ? 256.0 : 1024.0;
-  const int rc = spline_line_wave(dm, R->n_out, b0, b1, W, lane, s_y, s_m, s_ct, [&](int o, double v) {
+  const int rc = spline_block<FINAL_NT>(dm, R->n_out, b0, b1, W, 0, W, tid, S, [&](int o, double v) {
     double red = ((v * wow) - C.ire0) / C.hz_ire;
     red -= C.vsync_ire;
     double x = (red * scale_) + base;
@@ -442,16 +402,16 @@ extern "C" __global__ __launch_bounds__(64) void ldg_k_final_lines(
     out[o] = (uint16_t)x;
   });
   if (rc < 0) {
-    if (lane == 0) R->status = FS_TBC;
+    if (tid == 0) R->status = FS_TBC;
     return;
   }
-  // NTSC burst flag pixels (lanes 0 / 1 wrote pixels 0 / 1 above)
-  if (!pal && lane < 2 && row >= 1 && row < lc - 1) {
+  // NTSC burst flag pixels (threads 0 / 1 wrote pixels 0 / 1 above)
+  if (!pal && tid < 2 && row >= 1 && row < lc - 1) {
     const float bl = blevel[(int64_t)slot * MAX_LINES + row];
     const double hzs = 1700000 / 140.0;
-    if (lane == 0) out[0] = bl > 0 ? 16384 : 32768;
+    if (tid == 0) out[0] = bl > 0 ? 16384 : 32768;
     const double clevel = (1 / 1.45) / hzs;
-    if (lane == 1) out[1] = (uint16_t)(327.67 * clevel * fabs((double)bl));
+    if (tid == 1) out[1] = (uint16_t)(327.67 * clevel * fabs((double)bl));
   }
 }
 
