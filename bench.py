@@ -158,7 +158,8 @@ def main():
         'cpu_baseline': cpu,
         'checks': {'cav_framenr_consecutive': consecutive, 'synth_s': round(synth_s, 2),
                    'reads_decoded': dec.stats['reads'], 'reads_used': dec.stats['reads_used'],
-                   'batches': dec.stats['batches']},
+                   'batches': dec.stats['batches'], 'misses': dec.stats.get('misses', 0),
+                   'miss_sample': dec.stats.get('miss_log', [])[:12]},
     }
     print(json.dumps(line), flush=True)
     if dist is not None:

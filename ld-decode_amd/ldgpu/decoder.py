@@ -136,12 +136,14 @@ class GPUDecoder:
         self.log = log or (lambda *a: None)
         self.stats = {'batches': 0, 'reads': 0, 'reads_used': 0, 'gpu_s': 0.0, 'replay_s': 0.0}
         self.cap_bytes = None
+        self.cap_nsamples = None
         self.cache = {}            # (start, mtf) -> (slot, info)
         self.hints = {}            # start -> absolute next start (start + nextfieldoffset)
         self._hint_keys = []       # sorted starts with hints
         P, D = (6, 4004000) if self.sysp.name == 'NTSC' else (2, 1600000)
         self.period, self.period_samples = P, D          # exact at 40 MSPS: 3 NTSC / 1 PAL frames
         self.field_nom = int(round(self.rf.freq_hz / self.sysp.fps / 2))
+        self.trace = None          # diagnostics: planner steps (tools/miss_probe.py)
 
     # ---- capture ---------------------------------------------------------------
     def set_capture(self, data, fmt, device_ptr=None, nsamples=None):
@@ -177,8 +179,25 @@ class GPUDecoder:
                 nxt = start + (self.rf.freq_hz * 1)
         return nxt
 
+    def _hint_key(self, start):
+        import bisect
+        ks = self._hint_keys
+        i = bisect.bisect_left(ks, start - 4096)
+        best = None
+        while i < len(ks) and ks[i] <= start + 4096:
+            if best is None or abs(ks[i] - start) < abs(best - start):
+                best = ks[i]
+            i += 1
+        if best is None:
+            return None
+        nx, inf = self.hints[best]
+        return (best, nx, inf.status, inf.istop, inf.vbi_framenr, inf.nvsync, [tuple(inf.vsync[q]) for q in range(min(inf.nvsync, 3))])
+
     def _hint(self, start):
-        """Next start predicted from any decoded read within 4096 samples (sync peaks are signal-locked)."""
+        """(next start, field info) of the decoded read nearest `start` within 4096 samples, or None.
+
+        Sync peaks, field parity and VBI are signal-locked: a read a few samples
+        away sees the same field and lands on the same next-field position."""
         import bisect
         ks = self._hint_keys
         i = bisect.bisect_left(ks, start - 4096)
@@ -208,6 +227,8 @@ class GPUDecoder:
                     new.append(key)
                     if len(new) >= want:
                         return new, chain
+                    if self.cap_nsamples is not None and read_geometry(key[0])[2] + BLOCKLEN > self.cap_nsamples:
+                        return new, chain     # this read's last block passes the capture end (EOF)
                 if hit is not None:
                     chain.append(key)
                     info = hit[1]
@@ -220,26 +241,38 @@ class GPUDecoder:
                     clv = bool(info.vbi_isclv) if valid else isclv
                 else:
                     h = self._hint(key[0])
-                    if h is not None:
-                        nxt = h
-                    elif len(starts) >= self.period:
-                        nxt = starts[-self.period] + self.period_samples
+                    if h is not None and h[1].status == native.FS_VALID:
+                        # a decoded read of the same field: its next start, parity and VBI
+                        nxt, hinfo = h
+                        valid = True
+                        istop = bool(hinfo.istop)
+                        fnr = hinfo.vbi_framenr if hinfo.vbi_framenr != native.VBI_NONE else None
+                        clv = bool(hinfo.vbi_isclv)
                     else:
-                        nxt = key[0] + self.field_nom
-                    valid = True
-                    istop = (not prev_top) if prev_top is not None else self.sysp.topfirst
-                    fnr = (fr + 1) if (fr is not None and not isclv) else None
-                    clv = isclv
-                starts.append(key[0])
+                        if h is not None:
+                            nxt = h[0]
+                        elif len(starts) >= self.period - 1:
+                            # r_{k+1} = r_{k+1-P} + D (P fields span D samples exactly)
+                            nxt = starts[-(self.period - 1)] + self.period_samples
+                        else:
+                            nxt = key[0] + self.field_nom
+                        valid = True
+                        istop = (not prev_top) if prev_top is not None else self.sysp.topfirst
+                        fnr = (fr + 1) if (fr is not None and not isclv) else None
+                        clv = isclv
                 sample = nxt
                 if not valid:
                     continue
+                starts.append(key[0])          # valid field starts only (the periodic ones)
                 prev_top = istop
                 if istop == self.sysp.topfirst:
                     fieldcount = 1
                 elif fieldcount == 1:
                     fieldcount = 2
                 last = (fnr, clv)
+                if self.trace is not None:
+                    hk = None if hit is not None else self._hint_key(key[0])
+                    self.trace.append((key, hit is not None, istop, fnr, fieldcount, nxt, hk))
             if last is None:
                 break
             fnr, clv = last
@@ -276,7 +309,7 @@ class GPUDecoder:
             if inf.status in (native.FS_VALID, native.FS_SHORT):
                 if k[0] not in self.hints:
                     bisect.insort(self._hint_keys, k[0])
-                self.hints[k[0]] = k[0] + inf.nextfieldoffset
+                self.hints[k[0]] = (k[0] + inf.nextfieldoffset, inf)
         if len(self._hint_keys) > 4096:           # keep the hint index bounded
             for s in self._hint_keys[:-2048]:
                 self.hints.pop(s, None)
@@ -400,8 +433,11 @@ class GPUDecoder:
         hist = []
         W, H = self.sysp.outlinelen, self.sysp.frame_lines
         while done < num_frames and self._tell() + bpf * 1.05 <= size:
+            # nothing known about this capture yet: learn the first fields' parity,
+            # VBI and sync positions from a small launch before speculating wide
+            want = self.batch if self._hint_keys else min(self.batch, 4)
             plan, chain = self._plan(nextsample, self.mtf_level, self.last_framenr, self.last_isclv, done == 0,
-                                     self.batch, hist)
+                                     want, hist)
             if plan:
                 self._launch(plan, set(chain))
             frames = []
@@ -426,7 +462,7 @@ class GPUDecoder:
                 fr.index = done + len(frames)
                 frames.append(fr)
                 nextsample = fr.nextsample
-                hist = (hist + [x.readsample for x in self.field_log])[-16:]
+                hist = (hist + [x.readsample for x in self.field_log if x.valid])[-16:]
             self.stats['replay_s'] += time.perf_counter() - t0
             self._flush(frames, W, H, sink)
             done += len(frames)
