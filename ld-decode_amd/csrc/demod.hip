@@ -97,6 +97,21 @@ __device__ __forceinline__ void split_pairs(CBuf x, const double2* __restrict__ 
   }
 }
 
+// Write merge(D * G) for my pairs (registers) into LDS (input of a C2R inverse FFT).
+__device__ __forceinline__ void merge_pairs(CBuf x, const double2* __restrict__ tw, const double2* __restrict__ G,
+                                            int tid, const Pairs& D) {
+  tid = fresh(tid);
+#pragma unroll
+  for (int q = 0; q < 5; q++) {
+    if (!pair_live(tid, q)) continue;
+    const int k = pair_k(tid, q), kp = M - k;
+    const double2 Pk = cmul(D.a[q], G[k]);
+    const double2 Pkp = cmul(D.b[q], G[kp]);
+    x[k] = cmerge(Pk, Pkp, tw[k]);
+    if (kp < M && kp != k) x[kp] = cmerge(Pkp, Pk, tw[kp]);
+  }
+}
+
 // Split the real-signal spectrum in LDS and park my pairs in global memory
 // (slot 2q: bin k, slot 2q+1: bin M-k; coalesced, this lane's own entries).
 __device__ __forceinline__ void park_split(CBuf x, const double2* __restrict__ tw, int tid, double2* __restrict__ park) {
@@ -281,12 +296,13 @@ extern "C" __global__ __launch_bounds__(1024) void ldg_k_demod(
     for (int q = 0; q < 8; q++) X_[tid + T * q] = make_double2(d0[q], d1[q]);
   }
   fft_lds<M, T, false>(X_, tw, tid);
-  park_split(X_, tw, tid, osp);
+  Pairs D;
+  split_pairs(X_, tw, tid, D);
   __syncthreads();
 
   const double inv = 1.0 / (double)M;
   auto emit = [&](int ch, const double2* G) {
-    merge_filtered(X_, tw, G, tid, osp);
+    merge_pairs(X_, tw, G, tid, D);
     fft_lds<M, T, true>(X_, tw, tid);
     double* o = vout + (int64_t)ch * vchan_stride;
     const int t = fresh(tid);
@@ -305,7 +321,7 @@ extern "C" __global__ __launch_bounds__(1024) void ldg_k_demod(
   if (C.n_chan > 4) emit(CH_PILOT, g_pilot);
 
   // ---- 6. 0.5 MHz channel (rolled by -F05_offset) and the sync detector --------
-  merge_filtered(X_, tw, g_05, tid, osp);
+  merge_pairs(X_, tw, g_05, tid, D);
   fft_lds<M, T, true>(X_, tw, tid);
   {
     double v0[8], v1[8];
@@ -329,7 +345,7 @@ extern "C" __global__ __launch_bounds__(1024) void ldg_k_demod(
     }
   }
   fft_lds<M, T, false>(X_, tw, tid);
-  park_split(X_, tw, tid, osp);
+  split_pairs(X_, tw, tid, D);
   __syncthreads();
   emit(CH_SYNC, g_psync);
 }
