@@ -26,6 +26,9 @@ NTSC_TBC_BYTES_PER_SAMPLE = 955500 / 1334667
 NTSC_PCM_BYTES_PER_SAMPLE = 0.0048
 BYTES_PER_SAMPLE = {0: 1.0, 1: 2.0, 2: 4 / 3, 3: 1.25}
 HBM_PEAK_GBS = 8000.0
+FP64_PEAK_TFLOPS = 78.6                           # MI355X FP64 vector (spec)
+READ_BLOCKS = 66                                  # overlap-save blocks per 1e6-sample field read
+DEMOD_FLOPS_PER_BLOCK = 9 * 5 * 8192 * 13 + 2 * 5 * 1024 * 10
 
 
 def parse():
@@ -94,6 +97,7 @@ def main():
             dist.barrier()
 
     dec.ctx.profile(True)
+    reads0 = dec.stats['reads']
     barrier()
     t0 = time.perf_counter()
     frames = 0
@@ -105,6 +109,7 @@ def main():
     dt = time.perf_counter() - t0
     stats = dec.ctx.profile_stats()
     dec.ctx.profile(False)
+    reads_timed = dec.stats['reads'] - reads0
     # sanity on the full-size output: consecutive CAV picture numbers, all frames present
     nrs = dec.frame_numbers
     consecutive = all(b == a + 1 for a, b in zip(nrs, nrs[1:]))
@@ -137,9 +142,19 @@ def main():
     pmc = os.path.join(ROOT, 'profiles', 'pmc_traffic.json')
     if os.path.exists(pmc):
         try:
-            traffic = json.load(open(pmc)).get(dom_name)
+            traffic = json.load(open(pmc))['kernels'].get(dom_name)
         except Exception:
             traffic = None
+    # secondary bound of the demod kernel: FP64 vector issue (FFT-convention
+    # flops 5 N log2 N: 9 x 8192-point + 2 x 1024-point complex FFTs per block)
+    fp64 = None
+    if 'demod' in stats and stats['demod'][0]:
+        blocks = reads_timed * READ_BLOCKS
+        flops = blocks * DEMOD_FLOPS_PER_BLOCK
+        tf = flops / (stats['demod'][1] * 1e-3) / 1e12
+        fp64 = {'kernel': 'demod', 'achieved_tflops': round(tf, 3), 'peak_tflops': FP64_PEAK_TFLOPS,
+                'frac': tf / FP64_PEAK_TFLOPS, 'flops_per_block': DEMOD_FLOPS_PER_BLOCK,
+                'blocks_per_launch': blocks / stats['demod'][0]}
     cpu = None if args.no_cpu else cpu_baseline(args.cpu_seconds)
     line = {
         'metric': 'RF Msamples/s (40 MSPS NTSC, full RF->.tbc decode)', 'value': round(msps, 3),
@@ -153,7 +168,8 @@ def main():
         'roofline': {'bound': 'hbm', 'kernel': dom_name, 'achieved': round(achieved, 4), 'peak': HBM_PEAK_GBS,
                      'unit': 'GB/s', 'frac': achieved / HBM_PEAK_GBS, 'traffic': traffic,
                      'avg_launch_ms': round(avg_ms, 4), 'launches': dom_launches,
-                     'algorithmic_bytes_per_sample': round(bps, 4)},
+                     'algorithmic_bytes_per_sample': round(bps, 4), 'traffic_unit': 'bytes per launch',
+                     'fp64': fp64},
         'kernels_ms': {k: round(v[1], 3) for k, v in sorted(stats.items(), key=lambda kv: -kv[1][1])},
         'cpu_baseline': cpu,
         'checks': {'cav_framenr_consecutive': consecutive, 'synth_s': round(synth_s, 2),

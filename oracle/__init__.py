@@ -12,7 +12,7 @@ Rules (DESIGN.md "Oracle"):
     checker / CPU baseline -- never as the thing measured or shipped.
   * The product (``ld-decode_amd/ldgpu``) never imports this package.
 
-Parity pinning: running the reference itself was denied in this environment
+PARITY UNPINNED (against the reference itself).  Running the reference was denied in this environment
 (binding), and the reference ships no tests, fixtures or golden
 vectors.  The restatement is therefore pinned by analytic
 known-answer tests derived from the reference source formulas (tests/
