@@ -159,9 +159,14 @@ int ldg_assemble_frames(ldg_ctx* ctx, int n, const int32_t* top_slots, const int
  * Copies up to `cap` bytes to host `dst`; returns bytes copied (>= 0) or an error. */
 int64_t ldg_debug_read(ldg_ctx* ctx, int slot, int what, void* dst, int64_t cap);
 
-/* 2D NTSC comb (comb-ntsc.cxx dim=2 defaults) on n 910x525 .tbc frames,
- * rgb48 744x480 out.  State (aburstlev, Y-NR FIR history) persists in ctx
- * across calls exactly as across frames of one reference comb process. */
+/* 2D NTSC comb (comb-ntsc.cxx dim=2 defaults, comb-ntsc.cxx:834-892) on n
+ * 910x525 .tbc frames, rgb48 744x480 out (the frames comb-ntsc writes to
+ * stdout, :704-733, :894-938).  State (the burst-level EMA aburstlev,
+ * :560-566) persists in ctx across calls exactly as across frames of one
+ * reference comb process; ldg_comb_reset starts a new process.
+ * io_is_device != 0: frames / rgb_out are device pointers; frames == NULL takes
+ * the context's frame buffer (ldg_assemble_frames with out == NULL), rgb_out ==
+ * NULL keeps the result in the context. */
 int ldg_comb_ntsc(ldg_ctx* ctx, int n, const uint16_t* frames, uint16_t* rgb_out, int io_is_device);
 int ldg_comb_reset(ldg_ctx* ctx);
 

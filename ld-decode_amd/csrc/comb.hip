@@ -1,8 +1,251 @@
-// 2D NTSC comb filter (comb-ntsc.cxx dim=2) -- placeholder until the kernel lands.
+// 2D NTSC comb filter: .tbc frames (910 x 525 uint16, 4fsc) -> rgb48 744 x 480.
+//
+// Restates comb-ntsc.cxx's default path (dim = 2, HQ colour LPF, nr_y = 1 IRE,
+// nr_c = 0, no pulldown): Comb::Process :834-892 -> Split1D :246-288, Split2D
+// :294-367, SplitIQ :414-483, AdjustY :735-763, FilterIQ :212-243, DoYNR
+// :523-553, ToRGB :555-598 (RGB::conv :124-147), PostProcess :894-938.
+//
+// Every output row depends only on its own line and the lines two above and
+// below it (the 2D stencil).  That holds with one exception: the burst-level
+// EMA `aburstlev` is a recurrence over all lines of all frames in order, so a
+// one-wave kernel runs that chain first.  DoYNR's FIR history crosses lines
+// and frames in the reference, but for output pixels (x >= 78) all 25 taps
+// fall inside the same line (h - 12 >= 66 >= 40), so the history never
+// reaches an output pixel.  One workgroup per (frame, output row) runs
+// SplitIQ -> AdjustY -> FilterIQ (two sequential 1-pole chains, as in the
+// reference) -> Y-NR -> YIQ->RGB with the row in LDS.
 #include <hip/hip_runtime.h>
 #include "common.hpp"
 
-struct ldg_ctx;
-void ldg_comb_free(ldg_ctx*) {}
-extern "C" int ldg_comb_ntsc(ldg_ctx*, int, const uint16_t*, uint16_t*, int) { return -4; }
-extern "C" int ldg_comb_reset(ldg_ctx*) { return 0; }
+namespace ldg {
+namespace comb {
+
+constexpr int IN_X = 910, IN_Y = 525;
+constexpr int OUT_W = 744, OUT_H = 480, OUT_X0 = 78, FIRST_LINE = 38;
+constexpr int CHAIN_LINES = IN_Y - FIRST_LINE;            // 487 lines feed aburstlev per frame
+constexpr double IRESCALE = 358.4, IREBASE = 1024.0;
+constexpr double BLACK_IRE = 7.5, BRIGHTNESS = 236.0;
+constexpr double NR_Y = 1.0 * IRESCALE;
+constexpr double P_2DRANGE = 45 * IRESCALE;
+constexpr double LPI_B0 = 2.267438981796600e-01, LPI_B1 = 2.267438981796600e-01;
+constexpr double LPI_A1 = -5.465122036406802e-01;
+
+struct NRTaps { double b[25]; };
+__constant__ NRTaps g_nr = {{
+    1.141291975113614e-04, -1.857019211291029e-03, -4.499636864042073e-03, -5.577680979937061e-03,
+    -4.423694440267179e-04, 1.309163063177155e-02,  2.861211356202848e-02,  3.029931283148555e-02,
+    1.098965697652802e-03,  -6.398130386469833e-02, -1.492080690537196e-01, -2.223459379380252e-01,
+    7.479077367478024e-01,  -2.223459379380252e-01, -1.492080690537196e-01, -6.398130386469833e-02,
+    1.098965697652803e-03,  3.029931283148557e-02,  2.861211356202848e-02,  1.309163063177156e-02,
+    -4.423694440267185e-04, -5.577680979937061e-03, -4.499636864042074e-03, -1.857019211291030e-03,
+    1.141291975113614e-04}};
+
+__device__ __forceinline__ double clampd(double v, double lo, double hi) { return v < lo ? lo : (v > hi ? hi : v); }
+
+// Split1D's tc1 of row r (0 outside lines 44..524 / pixels 4..839): integer average.
+__device__ __forceinline__ double clp0(const uint16_t* __restrict__ fr, int r, int h) {
+  if (r < 44 || r >= IN_Y || h < 4 || h >= 840) return 0.0;
+  const uint16_t* line = fr + r * IN_X;
+  const int avg = ((int)line[h + 2] + (int)line[h - 2]) / 2;
+  return (double)(avg - (int)line[h]);
+}
+
+// Split2D's adaptive 2D value at (l, h), l in [36, 524), h in [18, 840).
+__device__ __forceinline__ double clp1(const uint16_t* __restrict__ fr, int l, int h) {
+  const double c0 = clp0(fr, l, h), cm = clp0(fr, l, h - 1);
+  const double p0 = clp0(fr, l - 2, h), pm = clp0(fr, l - 2, h - 1);
+  const double n0 = clp0(fr, l + 2, h), nm = clp0(fr, l + 2, h - 1);
+  double kp = fabs(fabs(c0) - fabs(p0));
+  kp += fabs(fabs(cm) - fabs(pm));
+  kp -= (fabs(c0) + fabs(cm)) * .10;
+  double kn = fabs(fabs(c0) - fabs(n0));
+  kn += fabs(fabs(cm) - fabs(nm));
+  kn -= (fabs(c0) + fabs(nm)) * .10;
+  kp /= 2;
+  kn /= 2;
+  kp = clampd(1 - (kp / P_2DRANGE), 0, 1);
+  kn = clampd(1 - (kn / P_2DRANGE), 0, 1);
+  double sc = 1.0;
+  if (kn != 0 || kp != 0) {
+    if (kn > (3 * kp)) kp = 0;
+    else if (kp > (3 * kn)) kn = 0;
+    sc = (2.0 / (kn + kp));
+    if (sc < 1.0) sc = 1.0;
+  } else if ((fabs(fabs(p0) - fabs(n0)) - fabs((n0 + p0) * .2)) <= 0) {
+    kn = kp = 1;
+  }
+  double tc1 = ((c0 - p0) * kp * sc);
+  tc1 += ((c0 - n0) * kn * sc);
+  tc1 /= (2 * 2);
+  return tc1;
+}
+
+// SplitIQ's signed chroma sample at (l, h), before the I/Q hold:
+// cavg = (clp2*k2 + clp1*k1 + clp0*k0) / 2 with the dim-2 weights.
+__device__ __forceinline__ double cavg_at(const uint16_t* __restrict__ fr, int l, int h, bool invertphase) {
+  double cavg = 0;
+  cavg += 0.0 * 0.0;
+  if (l < 524 && h >= 18) {
+    cavg += clp1(fr, l, h) * 1.0;
+    cavg += clp0(fr, l, h) * 0.0;
+  } else {
+    cavg += 0.0 * 0.0;
+    cavg += clp0(fr, l, h) * 1.0;
+  }
+  cavg /= 2;
+  if (!invertphase) cavg = -cavg;
+  return cavg;
+}
+
+// u16_to_ire of a double passed as uint16_t (truncation to int32, low 16 bits)
+__device__ __forceinline__ double u16_to_ire_of(double v) {
+  const uint16_t level = (uint16_t)(int32_t)v;
+  if (level == 0) return -100;
+  return -40 + ((double)level - IREBASE) / IRESCALE;
+}
+
+}  // namespace comb
+}  // namespace ldg
+
+using namespace ldg::comb;
+
+// aburstlev chain (ToRGB :560-566) over lines 38..524 of n frames in order.
+// state[0]: aburstlev carried across calls (-1 = not initialised).
+// abl[f * CHAIN_LINES + (l - 38)]: the value ToRGB uses for line l of frame f.
+// grid: 1 workgroup of 64 threads.
+extern "C" __global__ __launch_bounds__(64) void ldg_k_comb_burst(const uint16_t* __restrict__ frames, int n,
+                                                                  double* __restrict__ state,
+                                                                  double* __restrict__ abl) {
+  const int lane = threadIdx.x;
+  double a = state[0];
+  const int total = n * CHAIN_LINES;
+  for (int c0 = 0; c0 < total; c0 += 64) {
+    const int j = c0 + lane;
+    double b = 0.0;
+    if (j < total) {
+      const int f = j / CHAIN_LINES, l = FIRST_LINE + j % CHAIN_LINES;
+      b = frames[(size_t)f * IN_X * IN_Y + (size_t)l * IN_X + 1] / IRESCALE;
+    }
+    double mine = 0.0;
+    const int cnt = (total - c0) < 64 ? (total - c0) : 64;
+    for (int k = 0; k < cnt; k++) {
+      const double bk = __shfl(b, k);
+      if (bk > 3) {
+        if (a < 0) a = bk;
+        a = (a * .99) + (bk * .01);
+      }
+      if (lane == k) mine = a;
+    }
+    if (j < total) abl[j] = mine;
+  }
+  if (lane == 0) state[0] = a;
+}
+
+// One output row: grid n * 480 workgroups of 256 threads; row r = line r + 38.
+extern "C" __global__ __launch_bounds__(256) void ldg_k_comb_rows(const uint16_t* __restrict__ frames,
+                                                                  const double* __restrict__ abl,
+                                                                  uint16_t* __restrict__ rgb) {
+  __shared__ double s_y[IN_X], s_i[IN_X], s_q[IN_X];    // SplitIQ cbuf, then AdjustY / FilterIQ in place
+  __shared__ double s_cv[IN_X];                          // signed chroma per pixel (before the hold)
+  const int tid = threadIdx.x;
+  const int f = blockIdx.x / OUT_H;
+  const int row = blockIdx.x % OUT_H;
+  const int l = row + FIRST_LINE;
+  const uint16_t* fr = frames + (size_t)f * IN_X * IN_Y;
+  const uint16_t* line = fr + (size_t)l * IN_X;
+  const bool invertphase = (line[0] == 16384);
+
+  // ---- SplitIQ: chroma samples, then the held I (even h) / Q (odd h) values
+  for (int h = tid; h < IN_X; h += 256) s_cv[h] = (h >= 4 && h < 840) ? cavg_at(fr, l, h, invertphase) : 0.0;
+  __syncthreads();
+  for (int h = tid; h < IN_X; h += 256) {
+    double y = 0, si = 0, sq = 0;
+    if (h >= 4 && h < 840) {
+      y = line[h];
+      const int he = h & ~1;                 // latest even h' <= h (phase 0 / 2)
+      si = ((he & 3) == 0) ? s_cv[he] : -s_cv[he];
+      const int ho = (h & 1) ? h : h - 1;    // latest odd h' <= h (phase 1 / 3), none before 5
+      if (ho >= 5) sq = ((ho & 3) == 1) ? -s_cv[ho] : s_cv[ho];
+    }
+    s_y[h] = y; s_i[h] = si; s_q[h] = sq;
+  }
+  __syncthreads();
+  // ---- AdjustY: p[h] = p[h + 2] with y += +-I / +-Q (h in [2, 842))
+  double ay[4], ai[4], aq[4];
+#pragma unroll
+  for (int e = 0; e < 4; e++) {
+    const int h = tid + 256 * e;
+    if (h >= IN_X) continue;
+    if (h >= 2 && h < 842) {
+      const double yy = s_y[h + 2], ii = s_i[h + 2], qq = s_q[h + 2];
+      double comp = 0;
+      switch (h & 3) {
+        case 0: comp = ii; break;
+        case 1: comp = -qq; break;
+        case 2: comp = -ii; break;
+        default: comp = qq; break;
+      }
+      if (invertphase) comp = -comp;
+      ay[e] = yy + comp; ai[e] = ii; aq[e] = qq;
+    } else {
+      ay[e] = s_y[h]; ai[e] = s_i[h]; aq[e] = s_q[h];
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int e = 0; e < 4; e++) {
+    const int h = tid + 256 * e;
+    if (h < IN_X) { s_y[h] = ay[e]; s_i[h] = ai[e]; s_q[h] = aq[e]; }
+  }
+  __syncthreads();
+  // ---- FilterIQ (lines >= 44): a fresh colorlpi IIR for I (even h) and for Q
+  //      (odd h), output two pixels back; thread 0 runs I, thread 64 runs Q
+  if (l >= 44 && (tid == 0 || tid == 64)) {
+    const bool isq = tid == 64;
+    double* src = isq ? s_q : s_i;
+    double x0 = 0, x1 = 0, y1 = 0, filt = 0;
+    for (int h = 4; h < 840; h++) {
+      if ((h & 1) == (isq ? 1 : 0)) {
+        x1 = x0;
+        x0 = src[h];
+        double y0 = 0;
+        y0 += (LPI_B0 / 1.0) * x0;
+        y0 += (LPI_B1 / 1.0) * x1;
+        y0 -= (LPI_A1 / 1.0) * y1;
+        y1 = y0;
+        filt = y0;
+      }
+      src[h - 2] = filt;           // reads of src[h] run ahead of these writes
+    }
+  }
+  __syncthreads();
+  // ---- DoYNR (taps inside this line for x >= 78) + ToRGB
+  const double aburst = abl[(size_t)f * CHAIN_LINES + (l - FIRST_LINE)];
+  const double m = BRIGHTNESS * 256 / 100;
+  uint16_t* out = rgb + ((size_t)f * OUT_H + row) * OUT_W * 3;
+  for (int x = tid; x < OUT_W; x += 256) {
+    const int h = x + OUT_X0;
+    double y0 = 0;
+#pragma unroll
+    for (int o = 0; o < 25; o++) y0 += (g_nr.b[o] / 1.0) * s_y[h + 12 - o];
+    double a = y0;
+    if (fabs(a) > NR_Y) a = (a > 0) ? NR_Y : -NR_Y;
+    const double yv = s_y[h] - a;
+    double iv = s_i[h], qv = s_q[h];
+    iv *= (10 / aburst);
+    qv *= (10 / aburst);
+    double y = u16_to_ire_of(yv);
+    y = (y - BLACK_IRE) * (100 / (100 - BLACK_IRE));
+    const double q = +(iv) / IRESCALE;
+    const double i = +(qv) / IRESCALE;
+    double r = y + (.956 * i) + (.621 * q);
+    double g = y - (.272 * i) - (.647 * q);
+    double b = y - (1.106 * i) + (1.703 * q);
+    r = clampd(r * m, 0, 65535);
+    g = clampd(g * m, 0, 65535);
+    b = clampd(b * m, 0, 65535);
+    out[x * 3 + 0] = (uint16_t)r;
+    out[x * 3 + 1] = (uint16_t)g;
+    out[x * 3 + 2] = (uint16_t)b;
+  }
+}

@@ -227,11 +227,21 @@ class Context:
         return a[:rc // a.itemsize]
 
     def comb_ntsc(self, frames):
+        """2D NTSC comb (comb-ntsc.cxx dim=2): n x (525, 910) uint16 frames -> n x (480, 744, 3) rgb48.
+        State (burst-level EMA) carries across calls like one reference comb process."""
         f = np.ascontiguousarray(frames, dtype=np.uint16).reshape(-1, 525 * 910)
-        out = np.zeros((f.shape[0], 480 * 744 * 3), dtype=np.uint16)
+        out = np.zeros((f.shape[0], 480, 744, 3), dtype=np.uint16)
         self._check(self.lib.ldg_comb_ntsc(self.h, f.shape[0], f.ctypes.data_as(C.c_void_p),
                                            out.ctypes.data_as(C.c_void_p), 0), 'ldg_comb_ntsc')
         return out
+
+    def comb_ntsc_device(self, n):
+        """Comb the first n frames of the context's device frame buffer (ldg_assemble_frames
+        with out=NULL) into the context's device rgb buffer (benchmark mode)."""
+        self._check(self.lib.ldg_comb_ntsc(self.h, n, None, None, 1), 'ldg_comb_ntsc')
+
+    def comb_reset(self):
+        self._check(self.lib.ldg_comb_reset(self.h), 'ldg_comb_reset')
 
     # ---- profiling / tooling -------------------------------------------------------
     def profile(self, on=True):

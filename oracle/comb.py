@@ -1,0 +1,47 @@
+"""ORACLE -- test infrastructure only.  ctypes wrapper of oracle/comb2d.cpp, the
+C++ restatement of the reference NTSC 2D comb (comb-ntsc.cxx dim=2 defaults).
+Built by oracle/Makefile into oracle/_build/libcomb2d.so."""
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB = os.path.join(HERE, '_build', 'libcomb2d.so')
+IN_X, IN_Y, OUT_W, OUT_H = 910, 525, 744, 480
+
+
+def _load():
+    if not os.path.exists(LIB) or os.path.getmtime(LIB) < os.path.getmtime(os.path.join(HERE, 'comb2d.cpp')):
+        subprocess.check_call(['make', '-s', '-C', HERE])
+    lib = C.CDLL(LIB)
+    lib.comb2d_create.restype = C.c_void_p
+    lib.comb2d_destroy.argtypes = [C.c_void_p]
+    lib.comb2d_process.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p]
+    lib.comb2d_aburstlev.argtypes = [C.c_void_p]
+    lib.comb2d_aburstlev.restype = C.c_double
+    return lib
+
+
+class Comb2D:
+    """One reference comb process: state (aburstlev, Y-NR FIR history) carries across calls."""
+
+    def __init__(self):
+        self.lib = _load()
+        self.h = self.lib.comb2d_create()
+
+    def __del__(self):
+        if getattr(self, 'h', None):
+            self.lib.comb2d_destroy(self.h)
+            self.h = None
+
+    def process(self, frames):
+        f = np.ascontiguousarray(frames, dtype=np.uint16).reshape(-1, IN_Y, IN_X)
+        out = np.zeros((f.shape[0], OUT_H, OUT_W, 3), dtype=np.uint16)
+        self.lib.comb2d_process(self.h, f.shape[0], f.ctypes.data, out.ctypes.data)
+        return out
+
+    @property
+    def aburstlev(self):
+        return self.lib.comb2d_aburstlev(self.h)

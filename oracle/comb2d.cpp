@@ -1,0 +1,249 @@
+// ORACLE -- TEST INFRASTRUCTURE ONLY.  C++ restatement of the reference NTSC
+// comb filter's default path (comb-ntsc.cxx, dim = 2, no pulldown, 16-bit
+// output) used as the checker for the GPU comb.  PARITY UNPINNED against the
+// reference binary itself (running it is denied; it also needs
+// OpenCV, absent here); pinned by known-answer tests in tests/test_comb.py.
+//
+// Built with -ffp-contract=off (oracle/Makefile): the reference's clang build
+// contracts or not depending on the compiler version, so the GPU tolerance is
+// +-1 LSB.  Stage map (reference file:line):
+//   Comb::Process (dim 2)           comb-ntsc.cxx:834-892
+//   Split1D                         :246-288   (clp0; its filtered tc1f is dim 1 only)
+//   Split2D                         :294-367   (clp1, combk)
+//   SplitIQ                         :414-483   (held I / Q samples)
+//   AdjustY                         :735-763
+//   FilterIQ                        :212-243   (fresh colorlpi IIR per line, HQ)
+//   VBI copy                        :870-877
+//   DoYNR                           :523-553   (persistent f_nr FIR across lines + frames)
+//   DoCNR                           :485-521   (nr_c = 0: no-op)
+//   ToRGB / RGB::conv / u16_to_ire  :555-598, :124-147, :116-121
+//   PostProcess + WriteFrame        :894-938, :704-733 (rows 38..517, x 78..821)
+//   Filter::feed (DF-I order)       ld-decoder.h:167-214
+//   f_nr, f_colorlpi constants      deemp.h:367-380, :425-432
+#include <cmath>
+#include <cstdint>
+#include <cstring>
+#include <vector>
+
+namespace {
+
+constexpr int IN_X = 910, IN_Y = 525;
+constexpr int OUT_W = 744, OUT_H = 480, OUT_X0 = 78, FIRST_LINE = 38;
+constexpr double IRESCALE = 358.4, IREBASE = 1024.0;
+constexpr double BLACK_IRE = 7.5, BRIGHTNESS = 236.0;
+constexpr double NR_Y = 1.0 * IRESCALE;      // main(): nr_y *= irescale
+constexpr double P_2DRANGE = 45 * IRESCALE;  // Split2D sets it per pixel
+
+// deemp.h f_nr (25-tap high pass used by DoYNR)
+const double NR_B[25] = {
+    1.141291975113614e-04, -1.857019211291029e-03, -4.499636864042073e-03, -5.577680979937061e-03,
+    -4.423694440267179e-04, 1.309163063177155e-02,  2.861211356202848e-02,  3.029931283148555e-02,
+    1.098965697652802e-03,  -6.398130386469833e-02, -1.492080690537196e-01, -2.223459379380252e-01,
+    7.479077367478024e-01,  -2.223459379380252e-01, -1.492080690537196e-01, -6.398130386469833e-02,
+    1.098965697652803e-03,  3.029931283148557e-02,  2.861211356202848e-02,  1.309163063177156e-02,
+    -4.423694440267185e-04, -5.577680979937061e-03, -4.499636864042074e-03, -1.857019211291030e-03,
+    1.141291975113614e-04};
+// deemp.h f_colorlpi (1-pole IIR; the HQ default uses it for I and Q)
+constexpr double LPI_B0 = 2.267438981796600e-01, LPI_B1 = 2.267438981796600e-01;
+constexpr double LPI_A1 = -5.465122036406802e-01;
+
+struct YIQ { double y = 0, i = 0, q = 0; };
+
+double clampd(double v, double lo, double hi) { return v < lo ? lo : (v > hi ? hi : v); }
+
+// u16_to_ire of a double passed where the reference takes uint16_t: the
+// implicit conversion truncates toward zero (x86: to int32, then the low 16 bits).
+double u16_to_ire_of(double v) {
+  const uint16_t level = (uint16_t)(int32_t)v;
+  if (level == 0) return -100;
+  return -40 + ((double)level - IREBASE) / IRESCALE;
+}
+
+struct Comb {
+  double aburstlev = -1;          // EMA of the burst level, global across frames
+  double nr_x[25] = {0};          // f_hpy input history x[0] newest, across lines and frames
+
+  double nr_feed(double v) {      // Filter::feed with a = {1}: y = sum_o (b[o] / 1.0) * x[o]
+    std::memmove(&nr_x[1], &nr_x[0], sizeof(double) * 24);
+    nr_x[0] = v;
+    double y0 = 0;
+    for (int o = 0; o < 25; o++) y0 += (NR_B[o] / 1.0) * nr_x[o];
+    return y0;
+  }
+
+  void process(const uint16_t* raw, uint16_t* rgb) {
+    // ---- Split1D: clp0 (lines 44..524), combk0 = 1 there
+    static double clp0[IN_Y + 2][IN_X], clp1[IN_Y][IN_X], k0[IN_Y][IN_X], k1[IN_Y][IN_X];
+    std::memset(clp0, 0, sizeof(clp0));
+    std::memset(clp1, 0, sizeof(clp1));
+    std::memset(k0, 0, sizeof(k0));
+    std::memset(k1, 0, sizeof(k1));
+    for (int l = 44; l < IN_Y; l++) {
+      const uint16_t* line = raw + l * IN_X;
+      for (int h = 4; h < 840; h++) {
+        const int avg = ((int)line[h + 2] + (int)line[h - 2]) / 2;   // integer /2
+        clp0[l][h] = (double)(avg - (int)line[h]);
+        k0[l][h] = 1;
+      }
+    }
+    // ---- Split2D (lines 36..524; 2D values for l < 524; n1line of l = 523
+    //      is row 525, which the reference reads as the zeroed next plane)
+    for (int l = 36; l < IN_Y; l++) {
+      const double* p1 = clp0[l - 2];
+      const double* c1 = clp0[l];
+      const double* n1 = clp0[l + 2];
+      if (l >= 4 && l < 524) {
+        for (int h = 18; h < 840; h++) {
+          double kp = std::fabs(std::fabs(c1[h]) - std::fabs(p1[h]));
+          kp += std::fabs(std::fabs(c1[h - 1]) - std::fabs(p1[h - 1]));
+          kp -= (std::fabs(c1[h]) + std::fabs(c1[h - 1])) * .10;
+          double kn = std::fabs(std::fabs(c1[h]) - std::fabs(n1[h]));
+          kn += std::fabs(std::fabs(c1[h - 1]) - std::fabs(n1[h - 1]));
+          kn -= (std::fabs(c1[h]) + std::fabs(n1[h - 1])) * .10;
+          kp /= 2;
+          kn /= 2;
+          kp = clampd(1 - (kp / P_2DRANGE), 0, 1);
+          kn = clampd(1 - (kn / P_2DRANGE), 0, 1);
+          double sc = 1.0;
+          if (kn != 0 || kp != 0) {
+            if (kn > (3 * kp)) kp = 0;
+            else if (kp > (3 * kn)) kn = 0;
+            sc = (2.0 / (kn + kp));
+            if (sc < 1.0) sc = 1.0;
+          } else if ((std::fabs(std::fabs(p1[h]) - std::fabs(n1[h])) - std::fabs((n1[h] + p1[h]) * .2)) <= 0) {
+            kn = kp = 1;
+          }
+          double tc1 = ((c1[h] - p1[h]) * kp * sc);
+          tc1 += ((c1[h] - n1[h]) * kn * sc);
+          tc1 /= (2 * 2);
+          clp1[l][h] = tc1;
+          k1[l][h] = 1.0;
+        }
+      }
+      for (int h = 4; h < 840; h++) {
+        // combk[1] *= 1 - combk[2] (combk[2] = 0 in 2D); combk[0] = 1 - combk[2] - combk[1]
+        k0[l][h] = 1 - 0.0 - k1[l][h];
+      }
+    }
+    // ---- SplitIQ -> cbuf (lines 36..524; everything else zero)
+    static YIQ cb[IN_Y][IN_X];
+    std::memset(cb, 0, sizeof(cb));
+    for (int l = 36; l < IN_Y; l++) {
+      const uint16_t* line = raw + l * IN_X;
+      const bool invertphase = (line[0] == 16384);
+      double si = 0, sq = 0;
+      for (int h = 4; h < 840; h++) {
+        double cavg = 0;
+        cavg += 0.0 * 0.0;               // clpbuffer[2] * combk[2]
+        cavg += clp1[l][h] * k1[l][h];
+        cavg += clp0[l][h] * k0[l][h];
+        cavg /= 2;
+        if (!invertphase) cavg = -cavg;
+        switch (h % 4) {
+          case 0: si = cavg; break;
+          case 1: sq = -cavg; break;
+          case 2: si = -cavg; break;
+          case 3: sq = cavg; break;
+        }
+        cb[l][h].y = line[h];
+        cb[l][h].i = si;
+        cb[l][h].q = sq;
+      }
+    }
+    // ---- AdjustY (lines 38..524): p[h] = p[h + 2] with y += +-I / +-Q
+    for (int l = FIRST_LINE; l < IN_Y; l++) {
+      const bool invertphase = (raw[l * IN_X] == 16384);
+      for (int h = 2; h < 842; h++) {
+        YIQ y = cb[l][h + 2];
+        double comp = 0;
+        switch (h % 4) {
+          case 0: comp = y.i; break;
+          case 1: comp = -y.q; break;
+          case 2: comp = -y.i; break;
+          case 3: comp = y.q; break;
+        }
+        if (invertphase) comp = -comp;
+        y.y += comp;
+        cb[l][h] = y;
+      }
+    }
+    // ---- FilterIQ (lines 44..524): fresh colorlpi for I and for Q per line, output 2 px back
+    for (int l = 44; l < IN_Y; l++) {
+      double xi[2] = {0, 0}, yi[2] = {0, 0}, xq[2] = {0, 0}, yq[2] = {0, 0};
+      auto feed = [](double* x, double* y, double v) {
+        x[1] = x[0]; y[1] = y[0];
+        x[0] = v;
+        double y0 = 0;
+        y0 += (LPI_B0 / 1.0) * x[0];
+        y0 += (LPI_B1 / 1.0) * x[1];
+        y0 -= (LPI_A1 / 1.0) * y[1];
+        y[0] = y0;
+        return y0;
+      };
+      double filti = 0, filtq = 0;
+      for (int h = 4; h < 840; h++) {
+        switch (h % 4) {
+          case 0: case 2: filti = feed(xi, yi, cb[l][h].i); break;
+          case 1: case 3: filtq = feed(xq, yq, cb[l][h].q); break;
+        }
+        cb[l][h - 2].i = filti;
+        cb[l][h - 2].q = filtq;
+      }
+    }
+    // (VBI copy into rows 0..23 and DoCNR do not reach the written rows)
+    // ---- DoYNR (lines 38..524): persistent FIR fed h = 40..843, output at h + 12
+    for (int l = FIRST_LINE; l < IN_Y; l++) {
+      double hp[IN_X + 32] = {0};
+      for (int h = 40; h <= 843; h++) hp[h] = nr_feed(cb[l][h].y);
+      for (int h = 40; h < 843; h++) {
+        double a = hp[h + 12];
+        if (std::fabs(a) > NR_Y) a = (a > 0) ? NR_Y : -NR_Y;
+        cb[l][h].y -= a;
+      }
+    }
+    // ---- ToRGB + PostProcess: rows 38..517, x 78..821
+    const double m = BRIGHTNESS * 256 / 100;
+    for (int l = FIRST_LINE; l < IN_Y; l++) {
+      const double burstlev = raw[l * IN_X + 1] / IRESCALE;
+      if (burstlev > 3) {
+        if (aburstlev < 0) aburstlev = burstlev;
+        aburstlev = (aburstlev * .99) + (burstlev * .01);
+      }
+      const int row = l - FIRST_LINE;
+      if (row >= OUT_H) continue;
+      for (int h = OUT_X0; h < OUT_X0 + OUT_W; h++) {
+        YIQ yiq = cb[l][h];
+        yiq.i *= (10 / aburstlev);
+        yiq.q *= (10 / aburstlev);
+        double y = u16_to_ire_of(yiq.y);
+        y = (y - BLACK_IRE) * (100 / (100 - BLACK_IRE));
+        const double q = +(yiq.i) / IRESCALE;
+        const double i = +(yiq.q) / IRESCALE;
+        double r = y + (.956 * i) + (.621 * q);
+        double g = y - (.272 * i) - (.647 * q);
+        double b = y - (1.106 * i) + (1.703 * q);
+        r = clampd(r * m, 0, 65535);
+        g = clampd(g * m, 0, 65535);
+        b = clampd(b * m, 0, 65535);
+        uint16_t* o = rgb + ((size_t)row * OUT_W + (h - OUT_X0)) * 3;
+        o[0] = (uint16_t)r;
+        o[1] = (uint16_t)g;
+        o[2] = (uint16_t)b;
+      }
+    }
+  }
+};
+
+}  // namespace
+
+extern "C" {
+void* comb2d_create() { return new Comb(); }
+void comb2d_destroy(void* c) { delete static_cast<Comb*>(c); }
+// n frames of 910 x 525 uint16 -> n frames of 744 x 480 x 3 uint16 (rgb48)
+void comb2d_process(void* c, int n, const uint16_t* frames, uint16_t* rgb) {
+  Comb* cb = static_cast<Comb*>(c);
+  for (int f = 0; f < n; f++)
+    cb->process(frames + (size_t)f * IN_X * IN_Y, rgb + (size_t)f * OUT_W * OUT_H * 3);
+}
+double comb2d_aburstlev(void* c) { return static_cast<Comb*>(c)->aburstlev; }
+}

@@ -21,6 +21,7 @@ import numpy as np  # noqa: E402
 
 from ldgpu.synth import make_capture  # noqa: E402
 from oracle.capture import FMT_BY_EXT, Capture  # noqa: E402
+from oracle.comb import Comb2D  # noqa: E402
 from oracle.demod import RFDemod  # noqa: E402
 from oracle.field import FieldNTSC  # noqa: E402
 from oracle.framer import decode_capture  # noqa: E402
@@ -50,6 +51,11 @@ def make(case):
     out = {'case': case, 'settings': {k: v for k, v in c.items()}, 'capture_sha256': sha(data),
            'frames': [{'tbc_sha256': sha(f.tobytes()), 'pcm_sha256': sha(a.tobytes()), 'pcm_len': int(a.size),
                        'meta': m} for f, a, m in zip(frames, pcm, meta)]}
+    if c['system'] == 'NTSC' and frames:
+        # the frames through the 2D comb restatement (one comb process, in order)
+        rgb = Comb2D().process(np.stack(frames))
+        for g, r in zip(out['frames'], rgb):
+            g['comb_rgb48_sha256'] = sha(r.tobytes())
     # per-stage vectors of the first valid field
     rf = RFDemod(system=c['system'])
     cap = Capture(data, fmt)

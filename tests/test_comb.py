@@ -1,0 +1,142 @@
+"""2D NTSC comb (comb-ntsc.cxx dim=2): oracle known-answer tests (CPU) and GPU parity.
+
+The oracle is oracle/comb2d.cpp, a C++ restatement of the reference comb's
+default path (PARITY UNPINNED against the reference binary, which cannot run
+here: SURVEY §8 C1/C2).  It is pinned here by closed-form answers:
+  * a flat grey field has no chroma: RGB = (IRE - 7.5) * 100/92.5 * 604.16;
+  * a solid-colour 4fsc field with NTSC line-to-line phase inversion decodes to
+    the I/Q it was built from (the 2D comb, the hold, AdjustY and the colour
+    LPF all have unit gain at DC);
+  * the burst-level EMA of a constant burst is that constant.
+GPU results must match the oracle within +-1 LSB.
+"""
+import numpy as np
+import pytest
+
+from oracle.comb import Comb2D
+
+IRESCALE, IREBASE = 358.4, 1024.0
+M = 236.0 * 256 / 100
+
+
+def ire_to_u16(ire):
+    return int(np.clip(((ire + 40) * IRESCALE) + IREBASE, 1, 65535))
+
+
+def frame_solid(y_ire, a=0, b=0, burst_ire=20.0):
+    """910x525 frame: luma y_ire plus a 4fsc chroma pattern c[h % 4] = (a, b, -a, -b),
+    sign flipping on every line of a field (frame rows l and l+2), burst flag/level in px 0/1."""
+    base = ire_to_u16(y_ire)
+    fr = np.zeros((525, 910), dtype=np.int64)
+    c = np.array([a, b, -a, -b], dtype=np.int64)
+    for l in range(525):
+        s = 1 if (l // 2) % 2 == 0 else -1
+        fr[l, :] = base + s * c[np.arange(910) % 4]
+        fr[l, 0] = 16384 if s > 0 else 32768
+        fr[l, 1] = int(burst_ire * IRESCALE)
+    return fr.astype(np.uint16)
+
+
+# deemp.h f_nr taps (DoYNR's high pass); its DC gain is not exactly 0, so a flat
+# field loses y * sum(taps) (clipped to +-1 IRE) -- the reference's behaviour.
+NR_B = [1.141291975113614e-04, -1.857019211291029e-03, -4.499636864042073e-03, -5.577680979937061e-03,
+        -4.423694440267179e-04, 1.309163063177155e-02, 2.861211356202848e-02, 3.029931283148555e-02,
+        1.098965697652802e-03, -6.398130386469833e-02, -1.492080690537196e-01, -2.223459379380252e-01,
+        7.479077367478024e-01, -2.223459379380252e-01, -1.492080690537196e-01, -6.398130386469833e-02,
+        1.098965697652803e-03, 3.029931283148557e-02, 2.861211356202848e-02, 1.309163063177156e-02,
+        -4.423694440267185e-04, -5.577680979937061e-03, -4.499636864042074e-03, -1.857019211291030e-03,
+        1.141291975113614e-04]
+
+
+def ynr(y_u16):
+    a = 0.0
+    for t in NR_B:
+        a += t * y_u16
+    return y_u16 - float(np.clip(a, -IRESCALE, IRESCALE))
+
+
+def expected_rgb(y_ire, i_val=0.0, q_val=0.0, burst_ire=20.0):
+    """RGB::conv (comb-ntsc.cxx:124-147) of y (u16, after DoYNR) and I/Q samples scaled by 10/aburstlev."""
+    yu = int(ynr(float(ire_to_u16(y_ire))))
+    y = -40 + (yu - IREBASE) / IRESCALE
+    y = (y - 7.5) * (100 / 92.5)
+    k = 10 / burst_ire
+    q = i_val * k / IRESCALE
+    i = q_val * k / IRESCALE
+    r = y + .956 * i + .621 * q
+    g = y - .272 * i - .647 * q
+    b = y - 1.106 * i + 1.703 * q
+    return np.clip(np.array([r, g, b]) * M, 0, 65535)
+
+
+def test_oracle_flat_grey_kat():
+    c = Comb2D()
+    out = c.process(frame_solid(50.0)[None])[0]
+    exp = expected_rgb(50.0)
+    core = out[20:460, 40:700].reshape(-1, 3).astype(np.float64)
+    assert np.abs(core - np.floor(exp)).max() <= 1
+    assert c.aburstlev == pytest.approx(20.0, rel=1e-12)
+
+
+@pytest.mark.parametrize('y_ire,a,b', [(40.0, 1500, -900), (60.0, -700, 1200), (25.0, 400, 400)])
+def test_oracle_solid_colour_kat(y_ire, a, b):
+    """A pattern c[h % 4] = (a, b, -a, -b) on rows flagged 16384 (the sign flipping
+    line to line within a field) decodes to the held samples I = -a, Q = b:
+    SplitIQ's phase table (:446-452) on the 2D comb output -c (:341-343)."""
+    out = Comb2D().process(frame_solid(y_ire, a, b)[None])[0].astype(np.float64)
+    core = out[40:440, 100:700].reshape(-1, 3)
+    assert np.abs(core - np.floor(expected_rgb(y_ire, -a, b))).max() <= 1
+    assert np.ptp(core.mean(0)) > 100          # a colour, not grey
+
+
+def test_oracle_state_carries_across_calls():
+    fr = np.stack([frame_solid(30.0, 800, 400, burst_ire=b) for b in (10.0, 25.0, 40.0)])
+    one = Comb2D().process(fr)
+    c = Comb2D()
+    two = np.concatenate([c.process(fr[:1]), c.process(fr[1:])])
+    assert np.array_equal(one, two)
+
+
+@pytest.mark.gpu
+def test_gpu_comb_matches_oracle(gpu_ctx_ntsc):
+    ctx, _ = gpu_ctx_ntsc
+    rng = np.random.default_rng(7)
+    frames = [frame_solid(40.0, 1500, -900), frame_solid(60.0, -700, 1200, burst_ire=30.0)]
+    noisy = frame_solid(50.0, 1000, 300).astype(np.int64) + rng.integers(-300, 300, (525, 910))
+    noisy[:, :2] = frame_solid(50.0)[:, :2]
+    frames.append(np.clip(noisy, 0, 65535).astype(np.uint16))
+    fr = np.stack(frames)
+    ctx.comb_reset()
+    g = np.concatenate([ctx.comb_ntsc(fr[:2]), ctx.comb_ntsc(fr[2:])])
+    o = Comb2D().process(fr)
+    d = np.abs(g.astype(np.int64) - o.astype(np.int64))
+    assert d.max() <= 1, d.max()
+    assert (d > 0).mean() < 1e-3
+
+
+@pytest.mark.gpu
+def test_gpu_comb_on_decoded_frames():
+    """RF -> .tbc on the GPU -> 2D comb on the GPU, against the oracle comb of the same
+    frames (+-1 LSB) and the committed golden comb hashes (bit-exact frames reported)."""
+    import hashlib
+    import json
+    import os
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    sys.path.insert(0, os.path.join(here, 'golden'))
+    import make_golden
+    from ldgpu.decoder import GPUDecoder
+    case = 'ntsc_cav_u8_0p2s'
+    with open(os.path.join(here, 'golden', case + '.json')) as fh:
+        gold = json.load(fh)
+    dec = GPUDecoder(system='NTSC', batch=8)
+    dec.set_capture(make_golden.build_capture(case), 0)
+    frames = []
+    dec.decode(sink=lambda fr, au, m: frames.append(fr.copy()))
+    fr = np.stack(frames).reshape(-1, 525, 910)
+    dec.ctx.comb_reset()
+    g = dec.ctx.comb_ntsc(fr)
+    o = Comb2D().process(fr)
+    assert np.abs(g.astype(np.int64) - o.astype(np.int64)).max() <= 1
+    exact = sum(hashlib.sha256(x.tobytes()).hexdigest() == e['comb_rgb48_sha256'] for x, e in zip(g, gold['frames']))
+    print('comb: %d/%d frames bit-identical to golden' % (exact, len(g)))

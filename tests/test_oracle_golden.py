@@ -34,6 +34,11 @@ def test_oracle_matches_golden(case):
         assert hashlib.sha256(f.tobytes()).hexdigest() == g['tbc_sha256']
         assert hashlib.sha256(a.tobytes()).hexdigest() == g['pcm_sha256']
         assert m == g['meta']
+    if frames and 'comb_rgb48_sha256' in gold['frames'][0]:
+        from oracle.comb import Comb2D
+        rgb = Comb2D().process(np.stack(frames))
+        assert [hashlib.sha256(r.tobytes()).hexdigest() for r in rgb] == \
+            [g['comb_rgb48_sha256'] for g in gold['frames']]
 
 
 def test_synthetic_vbi_frame_numbers():
