@@ -24,6 +24,7 @@ import numpy as np  # noqa: E402
 
 NTSC_TBC_BYTES_PER_SAMPLE = 955500 / 1334667
 NTSC_PCM_BYTES_PER_SAMPLE = 0.0048
+NTSC_COMB_BYTES_PER_SAMPLE = (955500 + 2142720) / 1334667   # .tbc in + rgb48 out per frame
 BYTES_PER_SAMPLE = {0: 1.0, 1: 2.0, 2: 4 / 3, 3: 1.25}
 HBM_PEAK_GBS = 8000.0
 FP64_PEAK_TFLOPS = 78.6                           # MI355X FP64 vector (spec)
@@ -41,6 +42,7 @@ def parse():
     ap.add_argument('--fmt', type=int, default=0)
     ap.add_argument('--cpu-seconds', type=float, default=0.3, help='oracle baseline sample (seconds of RF)')
     ap.add_argument('--no-cpu', action='store_true')
+    ap.add_argument('--no-comb', action='store_true', help='stop at .tbc (skip the 2D comb stage)')
     return ap.parse_args()
 
 
@@ -85,7 +87,7 @@ def main():
     synth_s = time.perf_counter() - t0
 
     def step():
-        return dec.decode(sink=None)
+        return dec.decode(sink=None, comb=not args.no_comb)
 
     for _ in range(args.warmup):
         nfr = step()
@@ -136,6 +138,8 @@ def main():
     dom_name, (dom_launches, dom_ms) = dom
     avg_ms = dom_ms / max(dom_launches, 1)
     bps = BYTES_PER_SAMPLE[args.fmt] + NTSC_TBC_BYTES_PER_SAMPLE + NTSC_PCM_BYTES_PER_SAMPLE
+    if not args.no_comb:
+        bps += NTSC_COMB_BYTES_PER_SAMPLE
     units_per_launch = (consumed / max(args.steps, 1)) / max(dom_launches / max(args.steps, 1), 1)
     achieved = bps * units_per_launch / (avg_ms * 1e-3) / 1e9
     traffic = None
@@ -161,7 +165,8 @@ def main():
         'unit': 'RF Msamples/s', 'n_gpus': world, 'steps': args.steps, 'warmup': args.warmup,
         'ms_per_step': round(dt_max / args.steps * 1e3, 3), 'higher_is_better': True, 'scaling': 'weak',
         'vs_baseline': None, 'dtype': 'f64', 'data': 'synthetic (GPU-synthesised NTSC CAV RF, u8)',
-        'config': {'workload': '%g s NTSC CAV, 40 MSPS 8-bit RF per GPU: RF->demod->TBC->.tbc+.pcm' % args.seconds,
+        'config': {'workload': '%g s NTSC CAV, 40 MSPS 8-bit RF per GPU: RF->demod->TBC->.tbc+.pcm%s'
+                               % (args.seconds, '' if args.no_comb else '->2D comb rgb48'),
                    'frames_per_step': frames // max(args.steps, 1), 'batch_reads': args.batch,
                    'parallelism': 'capture-sharded x%d' % world},
         'fields_per_s': round(fields_s, 1), 'realtime_x': round(msps / 40.0, 2),

@@ -50,11 +50,11 @@ __device__ __forceinline__ double clp0(const uint16_t* __restrict__ fr, int r, i
   return (double)(avg - (int)line[h]);
 }
 
-// Split2D's adaptive 2D value at (l, h), l in [36, 524), h in [18, 840).
-__device__ __forceinline__ double clp1(const uint16_t* __restrict__ fr, int l, int h) {
-  const double c0 = clp0(fr, l, h), cm = clp0(fr, l, h - 1);
-  const double p0 = clp0(fr, l - 2, h), pm = clp0(fr, l - 2, h - 1);
-  const double n0 = clp0(fr, l + 2, h), nm = clp0(fr, l + 2, h - 1);
+// clp1 with the three clp0 rows staged in LDS (p = l-2, c = l, n = l+2).
+__device__ __forceinline__ double clp1_lds(const double* p1, const double* c1, const double* n1, int h) {
+  const double c0 = c1[h], cm = c1[h - 1];
+  const double p0 = p1[h], pm = p1[h - 1];
+  const double n0 = n1[h], nm = n1[h - 1];
   double kp = fabs(fabs(c0) - fabs(p0));
   kp += fabs(fabs(cm) - fabs(pm));
   kp -= (fabs(c0) + fabs(cm)) * .10;
@@ -80,23 +80,6 @@ __device__ __forceinline__ double clp1(const uint16_t* __restrict__ fr, int l, i
   return tc1;
 }
 
-// SplitIQ's signed chroma sample at (l, h), before the I/Q hold:
-// cavg = (clp2*k2 + clp1*k1 + clp0*k0) / 2 with the dim-2 weights.
-__device__ __forceinline__ double cavg_at(const uint16_t* __restrict__ fr, int l, int h, bool invertphase) {
-  double cavg = 0;
-  cavg += 0.0 * 0.0;
-  if (l < 524 && h >= 18) {
-    cavg += clp1(fr, l, h) * 1.0;
-    cavg += clp0(fr, l, h) * 0.0;
-  } else {
-    cavg += 0.0 * 0.0;
-    cavg += clp0(fr, l, h) * 1.0;
-  }
-  cavg /= 2;
-  if (!invertphase) cavg = -cavg;
-  return cavg;
-}
-
 // u16_to_ire of a double passed as uint16_t (truncation to int32, low 16 bits)
 __device__ __forceinline__ double u16_to_ire_of(double v) {
   const uint16_t level = (uint16_t)(int32_t)v;
@@ -112,40 +95,52 @@ using namespace ldg::comb;
 // aburstlev chain (ToRGB :560-566) over lines 38..524 of n frames in order.
 // state[0]: aburstlev carried across calls (-1 = not initialised).
 // abl[f * CHAIN_LINES + (l - 38)]: the value ToRGB uses for line l of frame f.
-// grid: 1 workgroup of 64 threads.
-extern "C" __global__ __launch_bounds__(64) void ldg_k_comb_burst(const uint16_t* __restrict__ frames, int n,
-                                                                  double* __restrict__ state,
-                                                                  double* __restrict__ abl) {
-  const int lane = threadIdx.x;
+// The recurrence is exact and sequential: 256 threads stage the burst levels
+// of a chunk in LDS, thread 0 runs the chain over them (the loads are off the
+// dependency path, so it runs at the FP64 mul+add latency), all threads write
+// the results back.  grid: 1 workgroup of 256 threads.
+constexpr int BURST_CHUNK = 4096;
+extern "C" __global__ __launch_bounds__(256) void ldg_k_comb_burst(const uint16_t* __restrict__ frames, int n,
+                                                                   double* __restrict__ state,
+                                                                   double* __restrict__ abl) {
+  __shared__ double s_b[BURST_CHUNK];
+  __shared__ double s_a[BURST_CHUNK];
+  const int tid = threadIdx.x;
   double a = state[0];
   const int total = n * CHAIN_LINES;
-  for (int c0 = 0; c0 < total; c0 += 64) {
-    const int j = c0 + lane;
-    double b = 0.0;
-    if (j < total) {
+  for (int c0 = 0; c0 < total; c0 += BURST_CHUNK) {
+    const int cnt = (total - c0) < BURST_CHUNK ? (total - c0) : BURST_CHUNK;
+    for (int k = tid; k < cnt; k += 256) {
+      const int j = c0 + k;
       const int f = j / CHAIN_LINES, l = FIRST_LINE + j % CHAIN_LINES;
-      b = frames[(size_t)f * IN_X * IN_Y + (size_t)l * IN_X + 1] / IRESCALE;
+      s_b[k] = frames[(size_t)f * IN_X * IN_Y + (size_t)l * IN_X + 1] / IRESCALE;
     }
-    double mine = 0.0;
-    const int cnt = (total - c0) < 64 ? (total - c0) : 64;
-    for (int k = 0; k < cnt; k++) {
-      const double bk = __shfl(b, k);
-      if (bk > 3) {
-        if (a < 0) a = bk;
-        a = (a * .99) + (bk * .01);
+    __syncthreads();
+    if (tid == 0) {
+#pragma unroll 8
+      for (int k = 0; k < cnt; k++) {
+        const double bk = s_b[k];
+        if (bk > 3) {
+          if (a < 0) a = bk;
+          a = (a * .99) + (bk * .01);
+        }
+        s_a[k] = a;
       }
-      if (lane == k) mine = a;
     }
-    if (j < total) abl[j] = mine;
+    __syncthreads();
+    for (int k = tid; k < cnt; k += 256) abl[c0 + k] = s_a[k];
+    __syncthreads();
   }
-  if (lane == 0) state[0] = a;
+  if (tid == 0) state[0] = a;
 }
 
 // One output row: grid n * 480 workgroups of 256 threads; row r = line r + 38.
 extern "C" __global__ __launch_bounds__(256) void ldg_k_comb_rows(const uint16_t* __restrict__ frames,
                                                                   const double* __restrict__ abl,
                                                                   uint16_t* __restrict__ rgb) {
-  __shared__ double s_y[IN_X], s_i[IN_X], s_q[IN_X];    // SplitIQ cbuf, then AdjustY / FilterIQ in place
+  __shared__ double s_c[3][IN_X];                        // Split1D clp0 of rows l-2, l, l+2
+  __shared__ double s_y[IN_X], s_i[IN_X], s_q[IN_X];    // cbuf after SplitIQ / AdjustY
+  __shared__ double s_fi[IN_X], s_fq[IN_X];              // FilterIQ output
   __shared__ double s_cv[IN_X];                          // signed chroma per pixel (before the hold)
   const int tid = threadIdx.x;
   const int f = blockIdx.x / OUT_H;
@@ -155,8 +150,30 @@ extern "C" __global__ __launch_bounds__(256) void ldg_k_comb_rows(const uint16_t
   const uint16_t* line = fr + (size_t)l * IN_X;
   const bool invertphase = (line[0] == 16384);
 
-  // ---- SplitIQ: chroma samples, then the held I (even h) / Q (odd h) values
-  for (int h = tid; h < IN_X; h += 256) s_cv[h] = (h >= 4 && h < 840) ? cavg_at(fr, l, h, invertphase) : 0.0;
+  for (int h = tid; h < IN_X; h += 256) {
+#pragma unroll
+    for (int k = 0; k < 3; k++) s_c[k][h] = clp0(fr, l - 2 + 2 * k, h);
+  }
+  __syncthreads();
+  // ---- SplitIQ: chroma samples (Split2D / Split1D weights), then the held I / Q
+  for (int h = tid; h < IN_X; h += 256) {
+    double cv = 0.0;
+    if (h >= 4 && h < 840) {
+      double cavg = 0;
+      cavg += 0.0 * 0.0;                                 // clpbuffer[2] * combk[2]
+      if (l < 524 && h >= 18) {
+        cavg += clp1_lds(s_c[0], s_c[1], s_c[2], h) * 1.0;
+        cavg += s_c[1][h] * 0.0;
+      } else {
+        cavg += 0.0 * 0.0;
+        cavg += s_c[1][h] * 1.0;
+      }
+      cavg /= 2;
+      if (!invertphase) cavg = -cavg;
+      cv = cavg;
+    }
+    s_cv[h] = cv;
+  }
   __syncthreads();
   for (int h = tid; h < IN_X; h += 256) {
     double y = 0, si = 0, sq = 0;
@@ -195,27 +212,29 @@ extern "C" __global__ __launch_bounds__(256) void ldg_k_comb_rows(const uint16_t
 #pragma unroll
   for (int e = 0; e < 4; e++) {
     const int h = tid + 256 * e;
-    if (h < IN_X) { s_y[h] = ay[e]; s_i[h] = ai[e]; s_q[h] = aq[e]; }
+    if (h < IN_X) { s_y[h] = ay[e]; s_i[h] = ai[e]; s_q[h] = aq[e]; s_fi[h] = ai[e]; s_fq[h] = aq[e]; }
   }
   __syncthreads();
-  // ---- FilterIQ (lines >= 44): a fresh colorlpi IIR for I (even h) and for Q
-  //      (odd h), output two pixels back; thread 0 runs I, thread 64 runs Q
+  // ---- FilterIQ (lines >= 44): a fresh colorlpi IIR for I (fed at even h) and
+  //      for Q (odd h); every h writes the latest output two pixels back, so
+  //      each feed at h fills positions h-2 and h-1.  Thread 0: I, thread 64: Q.
   if (l >= 44 && (tid == 0 || tid == 64)) {
     const bool isq = tid == 64;
-    double* src = isq ? s_q : s_i;
-    double x0 = 0, x1 = 0, y1 = 0, filt = 0;
-    for (int h = 4; h < 840; h++) {
-      if ((h & 1) == (isq ? 1 : 0)) {
-        x1 = x0;
-        x0 = src[h];
-        double y0 = 0;
-        y0 += (LPI_B0 / 1.0) * x0;
-        y0 += (LPI_B1 / 1.0) * x1;
-        y0 -= (LPI_A1 / 1.0) * y1;
-        y1 = y0;
-        filt = y0;
-      }
-      src[h - 2] = filt;           // reads of src[h] run ahead of these writes
+    const double* src = isq ? s_q : s_i;
+    double* dst = isq ? s_fq : s_fi;
+    double x0 = 0, x1 = 0, y1 = 0;
+    if (isq) dst[2] = 0.0;                 // h = 4 writes the not-yet-fed Q output
+#pragma unroll 4
+    for (int h = isq ? 5 : 4; h < 840; h += 2) {
+      x1 = x0;
+      x0 = src[h];
+      double y0 = 0;
+      y0 += (LPI_B0 / 1.0) * x0;
+      y0 += (LPI_B1 / 1.0) * x1;
+      y0 -= (LPI_A1 / 1.0) * y1;
+      y1 = y0;
+      dst[h - 2] = y0;
+      if (h + 1 < 840) dst[h - 1] = y0;
     }
   }
   __syncthreads();
@@ -231,7 +250,7 @@ extern "C" __global__ __launch_bounds__(256) void ldg_k_comb_rows(const uint16_t
     double a = y0;
     if (fabs(a) > NR_Y) a = (a > 0) ? NR_Y : -NR_Y;
     const double yv = s_y[h] - a;
-    double iv = s_i[h], qv = s_q[h];
+    double iv = s_fi[h], qv = s_fq[h];
     iv *= (10 / aburst);
     qv *= (10 / aburst);
     double y = u16_to_ire_of(yv);

@@ -1,0 +1,118 @@
+#!/usr/bin/env python3
+"""lddecode.py on the MI355X: the reference CLI (lddecode.py:16-107) with the RF
+decode, TBC and (optionally) the 2D NTSC comb on the GPU.
+
+    python ld-decode_amd/lddecode.py [-s N] [-S N] [-E N] [-l N] [-p|-n] [-c] infile outfile
+
+Same arguments, loader selection by extension (.lds / .r30 / .r16, else 8-bit),
+the same frame accounting (samples_per_frame = int(fs/FPS)+1, the 10-bit
+bytes_per_frame and the fd.tell() + 1.05 frame EOF guard), `frame <n>` lines,
+and the same outputs: <outfile>.tbc (native uint16 frames) and <outfile>.pcm
+(int16 stereo, 48 kHz); cut mode (-c) writes <outfile>.r16.  Additions:
+<outfile>.json (per-frame VBI and per-field metadata, one JSON list) and
+--comb (<outfile>.rgb: comb-ntsc's default rgb48 744x480 frames).
+"""
+import argparse
+import json
+import os
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+
+import numpy as np  # noqa: E402
+
+from ldgpu.decoder import GPUDecoder  # noqa: E402
+from ldgpu.formats import fmt_from_path, read_samples, samples_in_bytes  # noqa: E402
+
+
+def parse(argv=None):
+    p = argparse.ArgumentParser(description='Extracts audio and video from raw RF laserdisc captures')
+    p.add_argument('infile', metavar='infile', type=str, help='source file')
+    p.add_argument('outfile', metavar='outfile', type=str, help='base name for destination files')
+    p.add_argument('-s', '--start', metavar='start', type=int, default=0,
+                   help='rough jump to frame n of capture (default is 0)')
+    p.add_argument('-S', '--seek', metavar='seek', type=int, default=-1, help='seek to frame n of capture')
+    p.add_argument('-E', '--end', metavar='end', type=int, default=-1, help='cutting: last frame')
+    p.add_argument('-l', '--length', metavar='length', type=int, help='limit length to n frames')
+    p.add_argument('-p', '--pal', dest='pal', action='store_true', help='source is in PAL format')
+    p.add_argument('-n', '--ntsc', dest='ntsc', action='store_true', help='source is in NTSC format')
+    p.add_argument('-c', '--cut', dest='cut', action='store_true', help='cut (to r16) instead of decode')
+    # MI355X additions
+    p.add_argument('--device', type=int, default=0, help='HIP device')
+    p.add_argument('--batch', type=int, default=64, help='field reads per GPU launch')
+    p.add_argument('--comb', action='store_true', help='also write <outfile>.rgb through the 2D NTSC comb')
+    p.add_argument('--no-json', action='store_true', help='do not write <outfile>.json')
+    return p.parse_args(argv)
+
+
+def main(argv=None):
+    args = parse(argv)
+    print(args)
+    filename, outname = args.infile, args.outfile
+    firstframe, req_frames = args.start, args.length
+    if args.pal and args.ntsc:
+        print("ERROR: Can only be PAL or NTSC")
+        return 1
+    system = 'PAL' if args.pal else 'NTSC'
+    if args.comb and system != 'NTSC':
+        print("ERROR: --comb is NTSC only")
+        return 1
+
+    dec = GPUDecoder(system=system, device=args.device, batch=args.batch)
+    samples_per_frame = dec.rf.samples_per_frame                 # int(fs / FPS) + 1
+    bytes_per_frame = samples_per_frame * 5 // 4                 # for 10-bit packed files
+    infile_size = os.path.getsize(filename)
+    if (infile_size // bytes_per_frame - firstframe) < 2:
+        print('Error: start frame is past end of file')
+        return 1
+
+    fmt = fmt_from_path(filename)
+    raw = np.memmap(filename, dtype=np.uint8, mode='r')
+    dec.set_capture(raw, fmt)
+
+    if args.seek >= 0:
+        nextsample = dec.findframe(args.seek, firstframe * samples_per_frame)
+    else:
+        nextsample = firstframe * samples_per_frame
+
+    if args.cut:
+        print(args.seek, args.end)
+        lastsample = dec.findframe(args.end, nextsample)
+        lastsample += int(samples_per_frame * .25)
+        total = samples_in_bytes(fmt, infile_size)
+        with open(outname + '.r16', 'wb') as out:
+            for i in range(nextsample, lastsample, 16384):
+                n = min(16384, lastsample - i, max(0, total - i))
+                out.write(read_samples(raw, fmt, i, n).astype(np.int16).tobytes())
+        return 0
+
+    num_frames = req_frames if req_frames is not None else infile_size // bytes_per_frame - firstframe
+    tbc = open(outname + '.tbc', 'wb')
+    pcm = open(outname + '.pcm', 'wb')
+    rgb = open(outname + '.rgb', 'wb') if args.comb else None
+    meta_all = []
+
+    def sink(frame, audio, meta):
+        print('frame ', meta['vbi']['framenr'])
+        tbc.write(frame.tobytes())
+        pcm.write(audio.tobytes())
+        meta_all.append(meta)
+
+    n = dec.decode(start_frame=firstframe, length=num_frames, sink=sink, comb=args.comb,
+                   comb_sink=(lambda r: rgb.write(r.tobytes())) if rgb else None,
+                   start_sample=nextsample)
+    if req_frames is not None and n < req_frames:
+        print('Warning: end of file reached before requested number of frames were decoded')
+    tbc.close()
+    pcm.close()
+    if rgb:
+        rgb.close()
+    if not args.no_json:
+        with open(outname + '.json', 'w') as fh:
+            json.dump(meta_all, fh)
+    return 0
+
+
+if __name__ == '__main__':
+    sys.exit(main())

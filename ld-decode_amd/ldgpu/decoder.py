@@ -144,6 +144,7 @@ class GPUDecoder:
         self.period, self.period_samples = P, D          # exact at 40 MSPS: 3 NTSC / 1 PAL frames
         self.field_nom = int(round(self.rf.freq_hz / self.sysp.fps / 2))
         self.trace = None          # diagnostics: planner steps (tools/miss_probe.py)
+        self.comb, self.comb_sink = False, None
 
     # ---- capture ---------------------------------------------------------------
     def set_capture(self, data, fmt, device_ptr=None, nsamples=None):
@@ -370,8 +371,9 @@ class GPUDecoder:
             merged['framenr'] = merged['minutes'] * 60 * fps + merged['seconds'] * fps + merged['clvframe']
         return merged
 
-    def readframe(self, sample, firstframe=False):
-        """lddecode_core.py:1254-1311 (formatoutput/audio deferred to the batch flush)."""
+    def readframe(self, sample, firstframe=False, cav=False):
+        """lddecode_core.py:1254-1311 (formatoutput/audio deferred to the batch flush).
+        cav: the reference's CAV framing (:1273-1275), used by findframe."""
         fieldcount = 0
         fields = [None, None]
         audio = []
@@ -383,7 +385,8 @@ class GPUDecoder:
                     fields[0] = f
                 else:
                     fields[1] = f
-                if f.istop == self.sysp.topfirst:
+                if ((not cav and (f.istop == self.sysp.topfirst)) or
+                        (cav and (f.vbi['framenr'] or f.vbi['minutes']))):
                     fieldcount = 1
                 elif fieldcount == 1:
                     fieldcount = 2
@@ -406,8 +409,66 @@ class GPUDecoder:
             oldmtf = self.mtf_level
             self.mtf_level = newmtf
             if np.abs(newmtf - oldmtf) > .1:
-                return self.readframe(sample, firstframe)
+                return self.readframe(sample, firstframe, cav)
         return FrameOut(top=fields[0], bottom=fields[1], audio_fields=audio, vbi=vbi, nextsample=sample)
+
+    # ---- seek (lddecode_core.py:1338-1378) -----------------------------------------
+    _STATE = ('mtf_level', 'audio_offset', 'last_framenr', 'last_isclv', 'last_read', 'vbi')
+
+    def _resolve(self, fn):
+        """Run a replay step; decode whatever reads it misses (a few speculative reads
+        ahead of each) and re-run it from the same state until it completes."""
+        while True:
+            saved = {k: getattr(self, k, None) for k in self._STATE}
+            self.requested, self.field_log = [], []
+            try:
+                return fn()
+            except Miss as m:
+                for k, v in saved.items():
+                    setattr(self, k, v)
+                keys, _ = self._plan(m.key[0], m.key[1], self.last_framenr, self.last_isclv, False, 4, [])
+                if m.key not in keys:
+                    keys = [m.key] + keys[:3]
+                self._launch(keys, set())
+
+    def findframe(self, target, nextsample=0, log=print):
+        """Sample number of frame `target` (lddecode_core.py:1338-1378), on a fresh
+        framer (mtf 1, audio offset 0).  Returns None where the reference does."""
+        spf = int(self.rf.freq_hz / self.sysp.fps)
+        self.mtf_level, self.audio_offset = 1, 0
+        self.last_framenr, self.last_isclv, self.last_read = None, False, None
+        self.vbi = {'framenr': None}
+        iscav = False
+        tolerance = 0
+        rv = None
+        retry = 5
+        while self.vbi['framenr'] is None and retry:
+            rv = self._resolve(lambda: self.readframe(nextsample, False, cav=False))
+            if rv is None:
+                raise ReferenceCrash('findframe: end of capture (reference: TypeError on rv[2])')
+            log(rv.nextsample, self.vbi)
+            if self.vbi['isclv']:
+                tolerance = 1
+            else:
+                tolerance = 0
+                iscav = True
+            nextsample = rv.nextsample + (self.rf.freq_hz * 10)
+            retry -= 1
+        if retry == 0 and self.vbi['framenr'] is None:
+            log("SEEK ERROR: Unable to find a usable frame")
+            return None
+        retry = 5
+        while np.abs(target - self.vbi['framenr']) > tolerance and retry:
+            offset = (spf * (target - 1 - self.vbi['framenr']))
+            nextsample = rv.nextsample + offset
+            rv = self._resolve(lambda: self.readframe(nextsample, False, cav=iscav))
+            if rv is None:
+                raise ReferenceCrash('findframe: end of capture (reference: TypeError on rv[2])')
+            log(self.vbi)
+            retry -= 1
+        if np.abs(target - self.vbi['framenr']) > tolerance:
+            log("SEEK WARNING: seeked to frame {0} instead of {1}".format(self.vbi['framenr'], target))
+        return nextsample
 
     # ---- main loop (lddecode.py:39-107) ------------------------------------------
     def _tell(self):
@@ -415,10 +476,16 @@ class GPUDecoder:
             return 0
         return loader_tell(self.fmt, read_geometry(self.last_read)[2], self.cap_bytes)
 
-    def decode(self, start_frame=0, length=None, sink=None):
+    def decode(self, start_frame=0, length=None, sink=None, comb=False, comb_sink=None, start_sample=None):
         """Decode frames; sink(frame_u16, pcm_i16, meta) per frame (None: frames stay in HBM).
 
+        comb: also run the 2D NTSC comb (comb-ntsc.cxx dim=2) on every frame, in
+        order, as one comb process; comb_sink(rgb48) receives each 480x744x3
+        frame (None with sink=None: the rgb frames stay in HBM).
         Returns the number of frames decoded."""
+        self.comb, self.comb_sink = comb, comb_sink
+        if comb:
+            self.ctx.comb_reset()
         spf = self.rf.samples_per_frame
         bpf = spf * 5 // 4                     # (sic) 10-bit packing assumed, lddecode.py:42
         size = self.cap_bytes
@@ -428,7 +495,7 @@ class GPUDecoder:
         self.mtf_level, self.audio_offset = 1, 0
         self.last_framenr, self.last_isclv, self.last_read = None, False, None
         self.frame_numbers, self.pcm_samples, self.last_meta = [], 0, None
-        nextsample = start_frame * spf
+        nextsample = start_frame * spf if start_sample is None else start_sample
         done = 0
         hist = []
         W, H = self.sysp.outlinelen, self.sysp.frame_lines
@@ -477,11 +544,18 @@ class GPUDecoder:
         tops = [f.top.slot for f in frames]
         bots = [f.bottom.slot for f in frames]
         if sink is None:
-            # benchmark mode: .tbc frames stay in HBM
+            # benchmark mode: .tbc frames (and their comb output) stay in HBM
             self.ctx.assemble_frames_device(tops, bots)
             pics = None
+            if self.comb:
+                self.ctx.comb_ntsc_device(len(frames))
         else:
             pics = self.ctx.assemble_frames(tops, bots, W, H)
+            if self.comb:
+                rgb = self.ctx.comb_ntsc(pics)
+                if self.comb_sink:
+                    for r in rgb:
+                        self.comb_sink(r)
         af = [(fr_i, x) for fr_i, fr in enumerate(frames) for x in fr.audio_fields]
         if af:
             pcm, counts, _ = self.ctx.field_audio([x.slot for _, x in af], [x.audio_offset for _, x in af])

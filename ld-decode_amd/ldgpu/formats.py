@@ -1,8 +1,9 @@
 """RF capture container formats (the loader plugin API's four formats).
 
 Byte layouts follow lddutils.py:131-229 (readers) and ddpack.c:11-29 (.r30
-writer).  These are host-side helpers for writing test/bench captures; the
-decode path unpacks on the GPU (csrc/unpack.hip).
+writer).  These are host-side helpers for writing test/bench captures and for
+the CLI's cut mode; the decode path unpacks on the GPU inside the demod kernel
+(csrc/demod.hip load_sample).
 """
 import numpy as np
 
@@ -52,3 +53,32 @@ def pack_lds(samples10):
     o[:, 3] = ((s[:, 2] & 0x3f) << 2) | (s[:, 3] >> 8)
     o[:, 4] = s[:, 3] & 0xff
     return o.tobytes()
+
+
+def read_samples(buf, fmt, sample, count):
+    """The loader plugin's ``loader(infile, sample, count)`` as int16 for a window
+    inside the capture (lddutils.py:131-229; the CLI cut mode, lddecode.py:73-78).
+    buf: the capture's bytes (ndarray of uint8, e.g. a np.memmap)."""
+    sample, count = int(sample), int(count)
+    if fmt == FMT_U8:
+        return np.asarray(buf[sample:sample + count], dtype=np.int16)
+    if fmt == FMT_S16:
+        return np.frombuffer(bytes(buf[2 * sample:2 * (sample + count)]), dtype='<i2').copy()
+    if fmt == FMT_R30:
+        w0, off = sample // 3, sample % 3
+        nw = (off + count + 2) // 3
+        words = np.frombuffer(bytes(buf[4 * w0:4 * (w0 + nw)]), dtype='<u4')
+        out = np.empty(words.size * 3, dtype=np.int16)
+        out[0::3] = words & 0x3ff
+        out[1::3] = (words >> 10) & 0x3ff
+        out[2::3] = (words >> 20) & 0x3ff
+        return out[off:off + count]
+    g0, off = sample // 4, sample % 4
+    ng = (off + count + 3) // 4
+    b = np.frombuffer(bytes(buf[5 * g0:5 * (g0 + ng)]), dtype=np.uint8).astype(np.uint16).reshape(-1, 5)
+    out = np.empty((b.shape[0], 4), dtype=np.int16)
+    out[:, 0] = (b[:, 0] << 2) | (b[:, 1] >> 6)
+    out[:, 1] = ((b[:, 1] & 0x3f) << 4) | (b[:, 2] >> 4)
+    out[:, 2] = ((b[:, 2] & 0x0f) << 6) | (b[:, 3] >> 2)
+    out[:, 3] = ((b[:, 3] & 0x03) << 8) | b[:, 4]
+    return out.reshape(-1)[off:off + count]

@@ -1,0 +1,99 @@
+"""lddecode.py CLI (lddecode.py:16-107 semantics) on the GPU decoder."""
+import hashlib
+import json
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+CLI = os.path.join(ROOT, 'ld-decode_amd', 'lddecode.py')
+
+
+def run_cli(*args):
+    return subprocess.run([sys.executable, CLI, *map(str, args)], capture_output=True, text=True, timeout=600)
+
+
+def test_cli_rejects_pal_and_ntsc(tmp_path):
+    r = run_cli('-p', '-n', tmp_path / 'x.u8', tmp_path / 'out')
+    assert 'ERROR: Can only be PAL or NTSC' in r.stdout and r.returncode == 1
+
+
+def test_cli_help_lists_reference_options():
+    r = run_cli('-h')
+    for opt in ('--start', '--seek', '--end', '--length', '--pal', '--ntsc', '--cut'):
+        assert opt in r.stdout
+
+
+def _golden_capture(tmp_path, case='ntsc_cav_u8_0p2s', ext='u8'):
+    sys.path.insert(0, os.path.join(HERE, 'golden'))
+    import make_golden
+    data = make_golden.build_capture(case)
+    path = tmp_path / ('cap.' + ext)
+    path.write_bytes(bytes(data))
+    with open(os.path.join(HERE, 'golden', case + '.json')) as fh:
+        return path, json.load(fh)
+
+
+@pytest.mark.gpu
+def test_cli_decode_matches_golden(tmp_path):
+    cap, gold = _golden_capture(tmp_path)
+    out = tmp_path / 'out'
+    r = run_cli(cap, out)
+    assert r.returncode == 0, r.stderr[-2000:]
+    frames = np.fromfile(str(out) + '.tbc', dtype=np.uint16).reshape(-1, 525, 910)
+    meta = json.load(open(str(out) + '.json'))
+    assert len(frames) == len(gold['frames']) == len(meta)
+    for m, g in zip(meta, gold['frames']):
+        assert m == g['meta']
+    pcm = np.fromfile(str(out) + '.pcm', dtype=np.int16)
+    assert pcm.size == sum(g['pcm_len'] for g in gold['frames'])
+    printed = [l for l in r.stdout.splitlines() if l.startswith('frame ')]
+    assert printed == ['frame  %s' % g['meta']['vbi']['framenr'] for g in gold['frames']]
+    exact = sum(hashlib.sha256(f.tobytes()).hexdigest() == g['tbc_sha256'] for f, g in zip(frames, gold['frames']))
+    print('CLI: %d/%d frames bit-identical' % (exact, len(frames)))
+
+
+@pytest.mark.gpu
+def test_cli_length_and_comb(tmp_path):
+    cap, gold = _golden_capture(tmp_path)
+    out = tmp_path / 'out'
+    r = run_cli('-l', 2, '--comb', cap, out)
+    assert r.returncode == 0, r.stderr[-2000:]
+    frames = np.fromfile(str(out) + '.tbc', dtype=np.uint16).reshape(-1, 525, 910)
+    rgb = np.fromfile(str(out) + '.rgb', dtype=np.uint16).reshape(-1, 480, 744, 3)
+    assert len(frames) == 2 and len(rgb) == 2
+    from oracle.comb import Comb2D
+    o = Comb2D().process(frames)
+    assert np.abs(o.astype(np.int64) - rgb.astype(np.int64)).max() <= 1
+
+
+@pytest.mark.gpu
+def test_cli_seek_and_cut(tmp_path):
+    """-S seeks by VBI frame number (findframe); -c writes the raw slice between two frames as .r16."""
+    sys.path.insert(0, os.path.join(HERE, 'golden'))
+    from ldgpu.synth import make_capture
+    data = make_capture(int(40e6 * 0.5), 'u8', first_frame=100, seed=11)
+    cap = tmp_path / 'cap.u8'
+    cap.write_bytes(bytes(data))
+    out = tmp_path / 'seek'
+    r = run_cli('-S', 105, '-l', 2, cap, out)
+    assert r.returncode == 0, r.stderr[-2000:]
+    meta = json.load(open(str(out) + '.json'))
+    assert [m['vbi']['framenr'] for m in meta] == [105, 106]
+    out = tmp_path / 'cut'
+    r = run_cli('-c', '-S', 103, '-E', 106, cap, out)
+    assert r.returncode == 0, r.stderr[-2000:]
+    r16 = np.fromfile(str(out) + '.r16', dtype=np.int16)
+    # the same seek in-process gives the slice bounds (lddecode.py:60-78)
+    from ldgpu.decoder import GPUDecoder
+    dec = GPUDecoder(system='NTSC', batch=8)
+    dec.set_capture(data, 0)
+    spf = dec.rf.samples_per_frame
+    first = dec.findframe(103, 0, log=lambda *a: None)
+    last = dec.findframe(106, first, log=lambda *a: None) + int(spf * .25)
+    raw = np.frombuffer(bytes(data), dtype=np.uint8).astype(np.int16)
+    assert np.array_equal(r16, raw[first:last])
