@@ -87,6 +87,7 @@ def main():
     synth_s = time.perf_counter() - t0
 
     def step():
+        dec.use_resident_capture(args.fmt, nsamp)      # fresh read cache: no reuse across steps
         return dec.decode(sink=None, comb=not args.no_comb)
 
     for _ in range(args.warmup):

@@ -289,15 +289,16 @@ class GPUDecoder:
         return new, chain
 
     def _launch(self, keys, protect):
-        """Decode `keys` into free slots (evicting cache entries not in `protect`)."""
-        used = {v[0] for k, v in self.cache.items() if k in protect}
+        """Decode `keys` into free slots, evicting least-recently-used cache entries
+        not in `protect` (the reads the replay is about to consume) as needed."""
+        used = {v[0] for v in self.cache.values()}
         free = [s for s in range(self.capacity) if s not in used]
         if len(free) < len(keys):
+            for k in [k for k in self.cache if k not in protect][:len(keys) - len(free)]:
+                free.append(self.cache.pop(k)[0])      # oldest first (insertion / touch order)
             keys = keys[:len(free)]
         if not keys:
             raise RuntimeError('read cache full (capacity %d)' % self.capacity)
-        for k in [k for k in self.cache if k not in protect]:
-            del self.cache[k]
         slots = free[:len(keys)]
         t0 = time.perf_counter()
         infos = self.ctx.decode_reads([k[0] for k in keys], [k[1] for k in keys], slots)
@@ -335,6 +336,7 @@ class GPUDecoder:
         hit = self.cache.get(key)
         if hit is None:
             raise Miss(key)
+        self.cache[key] = self.cache.pop(key)         # LRU touch
         slot, info = hit
         if info.status == native.FS_CRASH:
             raise ReferenceCrash('reference would raise at read %d' % readsample)
@@ -415,10 +417,10 @@ class GPUDecoder:
     # ---- seek (lddecode_core.py:1338-1378) -----------------------------------------
     _STATE = ('mtf_level', 'audio_offset', 'last_framenr', 'last_isclv', 'last_read', 'vbi')
 
-    def _resolve(self, fn):
+    def _resolve(self, fn, max_launches=64):
         """Run a replay step; decode whatever reads it misses (a few speculative reads
         ahead of each) and re-run it from the same state until it completes."""
-        while True:
+        for _ in range(max_launches):
             saved = {k: getattr(self, k, None) for k in self._STATE}
             self.requested, self.field_log = [], []
             try:
@@ -429,7 +431,8 @@ class GPUDecoder:
                 keys, _ = self._plan(m.key[0], m.key[1], self.last_framenr, self.last_isclv, False, 4, [])
                 if m.key not in keys:
                     keys = [m.key] + keys[:3]
-                self._launch(keys, set())
+                self._launch(keys, set(self.requested))
+        raise RuntimeError('replay step did not converge after %d launches' % max_launches)
 
     def findframe(self, target, nextsample=0, log=print):
         """Sample number of frame `target` (lddecode_core.py:1338-1378), on a fresh

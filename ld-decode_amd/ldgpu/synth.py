@@ -86,7 +86,7 @@ class SynthRF:
     """Chunked generator.  ``generate(n)`` returns float64 RF; ``encode`` quantises."""
 
     def __init__(self, system='NTSC', first_frame=1, clv=False, seed=20181015, noise=0.02,
-                 start_line=100, audio=True, bars=True):
+                 start_line=100, audio=True, bars=True, code_fields=(0, 1)):
         self.p = NTSC if system == 'NTSC' else PAL
         p = self.p
         self.spl = FS * p['line_us'] / 1e6          # samples per line (2542.22 / 2560)
@@ -94,6 +94,7 @@ class SynthRF:
         self.seed, self.noise, self.audio = seed, noise, audio
         self.t0_lines = start_line                  # capture starts this many lines into frame 0
         self.bars = bars
+        self.code_fields = tuple(code_fields)        # fields carrying the Philips codes
         self.b_emp, self.a_emp = emphasis_filter(p)
         # band-limit of the hard-edged baseband (windowed sinc, 4.4 MHz)
         self.fir = sps.firwin(63, 4.4e6 / (FS / 2))
@@ -178,7 +179,7 @@ class SynthRF:
             c = np.where(lower | (not self.bars), 0.0, camp[bar] * np.sin(w[act] + cph[bar]))
             ire[act] = y + c
         # Philips code lines
-        for fld in (0, 1):
+        for fld in self.code_fields:
             for j, cl in enumerate(p['code_lines'][fld]):
                 m = normal & (ln == cl)
                 if not np.any(m):

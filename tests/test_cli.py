@@ -76,7 +76,9 @@ def test_cli_seek_and_cut(tmp_path):
     """-S seeks by VBI frame number (findframe); -c writes the raw slice between two frames as .r16."""
     sys.path.insert(0, os.path.join(HERE, 'golden'))
     from ldgpu.synth import make_capture
-    data = make_capture(int(40e6 * 0.5), 'u8', first_frame=100, seed=11)
+    # picture numbers on the first field of each frame only: the reference's CAV
+    # framing in findframe (lddecode_core.py:1273-1275) needs a field without one
+    data = make_capture(int(40e6 * 0.5), 'u8', first_frame=100, seed=11, code_fields=(0,))
     cap = tmp_path / 'cap.u8'
     cap.write_bytes(bytes(data))
     out = tmp_path / 'seek'
