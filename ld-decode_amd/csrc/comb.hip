@@ -87,6 +87,36 @@ __device__ __forceinline__ double u16_to_ire_of(double v) {
   return -40 + ((double)level - IREBASE) / IRESCALE;
 }
 
+// FilterIQ's 1-pole colorlpi chain over one of I (even h) / Q (odd h): every h
+// writes the latest output two pixels back, so the feed at h fills h-2 and
+// h-1.  Inputs are prefetched 16 at a time so only the recurrence is serial.
+template <bool Q>
+__device__ __forceinline__ void iq_chain(const double* __restrict__ src, double* __restrict__ dst) {
+  double x0 = 0, x1 = 0, y1 = 0;
+  if (Q) dst[2] = 0.0;                     // h = 4 writes the not-yet-fed Q output
+  constexpr int H0 = Q ? 5 : 4;
+  for (int hb = H0; hb < 840; hb += 32) {
+    double xs[16];
+#pragma unroll
+    for (int k = 0; k < 16; k++) { const int h = hb + 2 * k; xs[k] = (h < 840) ? src[h] : 0.0; }
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+      const int h = hb + 2 * k;
+      if (h < 840) {
+        x1 = x0;
+        x0 = xs[k];
+        double y0 = 0;
+        y0 += (LPI_B0 / 1.0) * x0;
+        y0 += (LPI_B1 / 1.0) * x1;
+        y0 -= (LPI_A1 / 1.0) * y1;
+        y1 = y0;
+        dst[h - 2] = y0;
+        if (h + 1 < 840) dst[h - 1] = y0;
+      }
+    }
+  }
+}
+
 }  // namespace comb
 }  // namespace ldg
 
@@ -117,13 +147,21 @@ extern "C" __global__ __launch_bounds__(256) void ldg_k_comb_burst(const uint16_
     }
     __syncthreads();
     if (tid == 0) {
-#pragma unroll 8
-      for (int k = 0; k < cnt; k++) {
+      int k = 0;
+      for (; k < cnt && a < 0; k++) {       // until the first qualifying line sets it
         const double bk = s_b[k];
         if (bk > 3) {
-          if (a < 0) a = bk;
+          a = bk;
           a = (a * .99) + (bk * .01);
         }
+        s_a[k] = a;
+      }
+      // a > 0 from here on (burst levels > 3): only the EMA is on the serial path
+#pragma unroll 8
+      for (; k < cnt; k++) {
+        const double bk = s_b[k];
+        const double e = (a * .99) + (bk * .01);
+        a = (bk > 3) ? e : a;
         s_a[k] = a;
       }
     }
@@ -140,8 +178,9 @@ extern "C" __global__ __launch_bounds__(256) void ldg_k_comb_rows(const uint16_t
                                                                   uint16_t* __restrict__ rgb) {
   __shared__ double s_c[3][IN_X];                        // Split1D clp0 of rows l-2, l, l+2
   __shared__ double s_y[IN_X], s_i[IN_X], s_q[IN_X];    // cbuf after SplitIQ / AdjustY
-  __shared__ double s_fi[IN_X], s_fq[IN_X];              // FilterIQ output
   __shared__ double s_cv[IN_X];                          // signed chroma per pixel (before the hold)
+  double* const s_fi = s_c[0];                           // FilterIQ output (clp0 rows are dead by then)
+  double* const s_fq = s_c[1];
   const int tid = threadIdx.x;
   const int f = blockIdx.x / OUT_H;
   const int row = blockIdx.x % OUT_H;
@@ -218,24 +257,9 @@ extern "C" __global__ __launch_bounds__(256) void ldg_k_comb_rows(const uint16_t
   // ---- FilterIQ (lines >= 44): a fresh colorlpi IIR for I (fed at even h) and
   //      for Q (odd h); every h writes the latest output two pixels back, so
   //      each feed at h fills positions h-2 and h-1.  Thread 0: I, thread 64: Q.
-  if (l >= 44 && (tid == 0 || tid == 64)) {
-    const bool isq = tid == 64;
-    const double* src = isq ? s_q : s_i;
-    double* dst = isq ? s_fq : s_fi;
-    double x0 = 0, x1 = 0, y1 = 0;
-    if (isq) dst[2] = 0.0;                 // h = 4 writes the not-yet-fed Q output
-#pragma unroll 4
-    for (int h = isq ? 5 : 4; h < 840; h += 2) {
-      x1 = x0;
-      x0 = src[h];
-      double y0 = 0;
-      y0 += (LPI_B0 / 1.0) * x0;
-      y0 += (LPI_B1 / 1.0) * x1;
-      y0 -= (LPI_A1 / 1.0) * y1;
-      y1 = y0;
-      dst[h - 2] = y0;
-      if (h + 1 < 840) dst[h - 1] = y0;
-    }
+  if (l >= 44) {
+    if (tid == 0) iq_chain<false>(s_i, s_fi);
+    if (tid == 64) iq_chain<true>(s_q, s_fq);
   }
   __syncthreads();
   // ---- DoYNR (taps inside this line for x >= 78) + ToRGB
