@@ -169,6 +169,12 @@ int64_t ldg_debug_read(ldg_ctx* ctx, int slot, int what, void* dst, int64_t cap)
  * NULL keeps the result in the context. */
 int ldg_comb_ntsc(ldg_ctx* ctx, int n, const uint16_t* frames, uint16_t* rgb_out, int io_is_device);
 int ldg_comb_reset(ldg_ctx* ctx);
+/* Asynchronous form for a fused pipeline: comb the first n frames of the
+ * context's frame buffer into its rgb buffer on a second stream, overlapped
+ * with the next ldg_decode_reads; the next ldg_assemble_frames into the
+ * context buffer waits for it.  ldg_sync waits for all outstanding work. */
+int ldg_comb_ntsc_async(ldg_ctx* ctx, int n);
+int ldg_sync(ldg_ctx* ctx);
 
 /* ---- in-library kernel timing (HIP events on the context's stream) ------------- */
 typedef struct ldg_kernel_stat {

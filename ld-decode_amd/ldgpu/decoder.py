@@ -213,6 +213,11 @@ class GPUDecoder:
         """Simulate the replay from a frame checkpoint; return up to `want` undecoded keys it will need."""
         new, seen, chain = [], set(), []
         starts = list(hist)
+        # the replay stops once the last read's fd.tell() + 1.05 frames passes the
+        # file size (lddecode.py:89): plan at most the rest of that frame beyond it
+        bpf = self.rf.samples_per_frame * 5 // 4
+        limit = (self.cap_bytes - bpf * 1.05) if self.cap_bytes is not None else None
+        past_limit = 0
         sample, cur_mtf, fr = int(nextsample), mtf, last_framenr
         prev_top = None
         steps = 0
@@ -230,6 +235,10 @@ class GPUDecoder:
                         return new, chain
                     if self.cap_nsamples is not None and read_geometry(key[0])[2] + BLOCKLEN > self.cap_nsamples:
                         return new, chain     # this read's last block passes the capture end (EOF)
+                    if limit is not None and loader_tell(self.fmt, read_geometry(key[0])[2], self.cap_bytes) > limit:
+                        past_limit += 1
+                        if past_limit > 3:
+                            return new, chain
                 if hit is not None:
                     chain.append(key)
                     info = hit[1]
@@ -539,6 +548,7 @@ class GPUDecoder:
             self.stats['reads_used'] += sum(len(f.fields) for f in frames)
             if eof or (not frames and not plan):
                 break
+        self.ctx.sync()
         return done
 
     def _flush(self, frames, W, H, sink):
@@ -551,7 +561,7 @@ class GPUDecoder:
             self.ctx.assemble_frames_device(tops, bots)
             pics = None
             if self.comb:
-                self.ctx.comb_ntsc_device(len(frames))
+                self.ctx.comb_ntsc_async(len(frames))     # overlaps the next batch's decode
         else:
             pics = self.ctx.assemble_frames(tops, bots, W, H)
             if self.comb:

@@ -20,7 +20,7 @@ MAX_VSYNCS = 16
 EXPORTS = ['ldg_create', 'ldg_destroy', 'ldg_last_error', 'ldg_set_filters', 'ldg_set_capture',
            'ldg_decode_reads', 'ldg_field_audio', 'ldg_assemble_frames', 'ldg_debug_read',
            'ldg_comb_ntsc', 'ldg_comb_reset', 'ldg_version', 'ldg_device_count', 'ldg_profile_enable',
-           'ldg_profile_read', 'ldg_synth_capture', 'ldg_capture_download']
+           'ldg_profile_read', 'ldg_synth_capture', 'ldg_capture_download', 'ldg_comb_ntsc_async', 'ldg_sync']
 
 
 class FieldInfo(C.Structure):
@@ -93,6 +93,8 @@ def load(path=LIB_PATH):
     lib.ldg_debug_read.restype = C.c_int64
     lib.ldg_comb_ntsc.argtypes = [vp, C.c_int, vp, vp, C.c_int]
     lib.ldg_comb_reset.argtypes = [vp]
+    lib.ldg_comb_ntsc_async.argtypes = [vp, C.c_int]
+    lib.ldg_sync.argtypes = [vp]
     lib.ldg_profile_enable.argtypes = [vp, C.c_int]
     lib.ldg_profile_read.argtypes = [vp, C.POINTER(KernelStat), C.c_int]
     lib.ldg_synth_capture.argtypes = [vp, C.POINTER(SynthParams), C.POINTER(C.c_double), C.POINTER(C.c_double),
@@ -239,6 +241,13 @@ class Context:
         """Comb the first n frames of the context's device frame buffer (ldg_assemble_frames
         with out=NULL) into the context's device rgb buffer (benchmark mode)."""
         self._check(self.lib.ldg_comb_ntsc(self.h, n, None, None, 1), 'ldg_comb_ntsc')
+
+    def comb_ntsc_async(self, n):
+        """ldg_comb_ntsc_async: comb the context's first n device frames on the comb stream."""
+        self._check(self.lib.ldg_comb_ntsc_async(self.h, n), 'ldg_comb_ntsc_async')
+
+    def sync(self):
+        self._check(self.lib.ldg_sync(self.h), 'ldg_sync')
 
     def comb_reset(self):
         self._check(self.lib.ldg_comb_reset(self.h), 'ldg_comb_reset')
