@@ -514,7 +514,8 @@ class GPUDecoder:
         while done < num_frames and self._tell() + bpf * 1.05 <= size:
             # nothing known about this capture yet: learn the first fields' parity,
             # VBI and sync positions from a small launch before speculating wide
-            want = self.batch if self._hint_keys else min(self.batch, 4)
+            # (until P + 2 field starts are known the period extrapolation has nothing to use)
+            want = self.batch if len(hist) >= self.period + 2 else min(self.batch, 8 if self._hint_keys else 4)
             plan, chain = self._plan(nextsample, self.mtf_level, self.last_framenr, self.last_isclv, done == 0,
                                      want, hist)
             if plan:
