@@ -23,7 +23,7 @@ from ldgpu.synth import make_capture  # noqa: E402
 from oracle.capture import FMT_BY_EXT, Capture  # noqa: E402
 from oracle.comb import Comb2D  # noqa: E402
 from oracle.demod import RFDemod  # noqa: E402
-from oracle.field import FieldNTSC  # noqa: E402
+from oracle.field import FieldNTSC, FieldPAL  # noqa: E402
 from oracle.framer import decode_capture  # noqa: E402
 
 CASES = {
@@ -31,6 +31,8 @@ CASES = {
     'ntsc_clv_u8_0p2s': dict(seconds=0.2, fmt='u8', system='NTSC', kw={'clv': True, 'first_frame': 5399}),
     'ntsc_cav_r30_0p15s': dict(seconds=0.15, fmt='r30', system='NTSC', kw={'seed': 7}),
     'ntsc_cav_lds_0p15s': dict(seconds=0.15, fmt='lds', system='NTSC', kw={'seed': 8}),
+    'pal_clv_u8_0p2s': dict(seconds=0.2, fmt='u8', system='PAL',
+                            kw={'clv': True, 'first_frame': 3000, 'seed': 5}),
 }
 
 
@@ -61,7 +63,7 @@ def make(case):
     cap = Capture(data, fmt)
     first = next(fr for m in meta for fr in m['fields'] if fr['valid'])
     raw = rf.demod(cap, first['readsample'], 1000000, first['mtf_level'])
-    f = FieldNTSC(rf, raw, 0, audio_offset=0)
+    f = (FieldNTSC if c['system'] == 'NTSC' else FieldPAL)(rf, raw, 0, audio_offset=0)
     p = int(f.peaklist[20])
     out['stage'] = {'readsample': first['readsample'], 'mtf_level': first['mtf_level'], 'peak20': p,
                     'demod': raw[0]['demod'][p - 8:p + 8].tolist(),
@@ -69,7 +71,7 @@ def make(case):
                     'demod_sync': raw[0]['demod_sync'][p - 8:p + 8].tolist(),
                     'demod_burst': raw[0]['demod_burst'][p - 8:p + 8].tolist(),
                     'linelocs': [float(x) for x in f.linelocs[:12]],
-                    'burstlevel': [float(x) for x in f.burstlevel[:12]]}
+                    'burstlevel': [float(x) for x in getattr(f, 'burstlevel', [])[:12]]}
     path = os.path.join(HERE, case + '.json')
     with open(path, 'w') as fh:
         json.dump(out, fh, indent=1)

@@ -101,7 +101,7 @@ def test_tbc_lines_and_audio(decoded):
 
 
 @pytest.mark.parametrize('case', ['ntsc_cav_u8_0p2s', 'ntsc_clv_u8_0p2s', 'ntsc_cav_r30_0p15s',
-                                  'ntsc_cav_lds_0p15s'])
+                                  'ntsc_cav_lds_0p15s', 'pal_clv_u8_0p2s'])
 @pytest.mark.parametrize("batch", [3, 16])
 def test_end_to_end_vs_golden(case, batch):
     """Full decode (speculative batches) vs the oracle's committed golden output."""
