@@ -146,6 +146,16 @@ int ldg_decode_reads(ldg_ctx* ctx, int n, const int64_t* read_starts, const doub
 int ldg_field_audio(ldg_ctx* ctx, int n, const int32_t* slots, const double* offsets, int16_t* pcm,
                     int64_t pcm_stride, int32_t* counts, double* next_offsets);
 
+/* Field archive (field-group sharding): keep the inputs of
+ * ldg_field_audio of n live slots (field record, final line locations, 625 kHz
+ * audio) at archive entries first..first+n-1, so a field's 48 kHz audio can be
+ * computed after its read slot is reused -- once a shard learns its exact
+ * starting audio time offset from the shards before it. */
+int ldg_archive_fields(ldg_ctx* ctx, int n, const int32_t* slots, int64_t first);
+/* ldg_field_audio over archive entries. */
+int ldg_archive_audio(ldg_ctx* ctx, int n, const int64_t* entries, const double* offsets, int16_t* pcm,
+                      int64_t pcm_stride, int32_t* counts, double* next_offsets);
+
 /* Interleave field pairs (top slot, bottom slot) into .tbc frames
  * (outlinelen x frame_lines uint16).  out_is_device: `out` is a device pointer. */
 int ldg_assemble_frames(ldg_ctx* ctx, int n, const int32_t* top_slots, const int32_t* bottom_slots,

@@ -423,17 +423,20 @@ extern "C" __global__ void ldg_k_finish(const int32_t* __restrict__ smap, FieldR
 
 // ---------------------------------------------------------------------------
 // downscale_audio (lddecode_core.py:431-484) for n fields.  grid: n x 256.
+// Field i's inputs live at entry idx[i] of (recs, lines + entry * lines_stride,
+// audio2 + entry * a2read_stride): the read slots (lines_stride LINES_STRIDE,
+// final locations at LLF) or the field archive (lines_stride MAX_LINES).
 extern "C" __global__ __launch_bounds__(256) void ldg_k_audio_ds(
-    const int32_t* __restrict__ slots, const double* __restrict__ offsets, const FieldRec* __restrict__ recs,
-    const double* __restrict__ lines, const double* __restrict__ audio2, int64_t a2read_stride,
+    const int64_t* __restrict__ idx, const double* __restrict__ offsets, const FieldRec* __restrict__ recs,
+    const double* __restrict__ lines, int64_t lines_stride, const double* __restrict__ audio2, int64_t a2read_stride,
     int64_t a2chan_stride, SysConst C, int16_t* __restrict__ pcm, int64_t pcm_stride, int32_t* __restrict__ counts,
     double* __restrict__ next_off, int32_t* __restrict__ err) {
   const int f = blockIdx.x;
-  const int slot = slots[f];
+  const int64_t slot = idx[f];
   const FieldRec* R = recs + slot;
   const int lc = R->linecount, nl = R->nlines;
-  const double* lf = lines + (int64_t)slot * LINES_STRIDE + LLF * MAX_LINES;
-  const double* aL = audio2 + (int64_t)slot * a2read_stride;
+  const double* lf = lines + slot * lines_stride;
+  const double* aL = audio2 + slot * a2read_stride;
   const double* aR = aL + a2chan_stride;
   const int64_t na = R->n_out > 0 ? ((R->n_out - 1) / AUDIO_DIV1 + 1) / AUDIO_DIV2 : 0;
   const double frametime = (C.line_period * lc) / 1000000;

@@ -67,7 +67,7 @@ class GPUField:
 
     __slots__ = ('info', 'slot', 'readsample', 'mtf_level', 'audio_offset', 'valid', 'istop', 'linecount',
                  'nextfieldoffset', 'npeaks', 'nvsync', 'vbi', 'linecode', 'tbcstart', 'status',
-                 'audio_next_offset', 'nextsample', 'dsaudio_used')
+                 'audio_next_offset', 'nextsample', 'dsaudio_used', 'tidx')
 
     def __init__(self, info, slot, readsample, mtf, audio_offset, sysp, frametime_lines):
         self.info, self.slot, self.readsample, self.mtf_level = info, slot, readsample, mtf
@@ -109,7 +109,7 @@ class GPUField:
 
 
 class FrameOut:
-    __slots__ = ('top', 'bottom', 'audio_fields', 'vbi', 'nextsample', 'fields', 'index')
+    __slots__ = ('top', 'bottom', 'audio_fields', 'vbi', 'nextsample', 'fields', 'index', 'start', 'tstart')
 
     def __init__(self, **kw):
         for k, v in kw.items():
@@ -145,6 +145,8 @@ class GPUDecoder:
         self.field_nom = int(round(self.rf.freq_hz / self.sysp.fps / 2))
         self.trace = None          # diagnostics: planner steps (tools/miss_probe.py)
         self.comb, self.comb_sink = False, None
+        self.transitions = []              # audio-offset chain: linecount of each transition's field
+        self.archive, self.arch_next, self.shard_frames = False, 0, []
 
     # ---- capture ---------------------------------------------------------------
     def set_capture(self, data, fmt, device_ptr=None, nsamples=None):
@@ -349,7 +351,9 @@ class GPUDecoder:
         slot, info = hit
         if info.status == native.FS_CRASH:
             raise ReferenceCrash('reference would raise at read %d' % readsample)
-        return GPUField(info, slot, int(readsample), mtf, audio_offset, self.sysp, None)
+        f = GPUField(info, slot, int(readsample), mtf, audio_offset, self.sysp, None)
+        f.tidx = len(self.transitions)       # audio-offset transitions before this field
+        return f
 
     def readfield(self, sample):
         """lddecode_core.py:1194-1223."""
@@ -408,6 +412,7 @@ class GPUDecoder:
             sample = nextsample
         if len(audio):
             self.audio_offset = f.audio_next_offset
+            self.transitions.append(int(f.linecount))   # offset -> next(offset, linecount)
         vbi = self.mergevbi(fields)
         self.vbi = vbi
         self.last_isclv = bool(f.vbi['isclv'])
@@ -431,12 +436,14 @@ class GPUDecoder:
         ahead of each) and re-run it from the same state until it completes."""
         for _ in range(max_launches):
             saved = {k: getattr(self, k, None) for k in self._STATE}
+            nt = len(self.transitions)
             self.requested, self.field_log = [], []
             try:
                 return fn()
             except Miss as m:
                 for k, v in saved.items():
                     setattr(self, k, v)
+                del self.transitions[nt:]
                 keys, _ = self._plan(m.key[0], m.key[1], self.last_framenr, self.last_isclv, False, 4, [])
                 if m.key not in keys:
                     keys = [m.key] + keys[:3]
@@ -450,6 +457,7 @@ class GPUDecoder:
         self.mtf_level, self.audio_offset = 1, 0
         self.last_framenr, self.last_isclv, self.last_read = None, False, None
         self.vbi = {'framenr': None}
+        self.transitions = []
         iscav = False
         tolerance = 0
         rv = None
@@ -488,14 +496,24 @@ class GPUDecoder:
             return 0
         return loader_tell(self.fmt, read_geometry(self.last_read)[2], self.cap_bytes)
 
-    def decode(self, start_frame=0, length=None, sink=None, comb=False, comb_sink=None, start_sample=None):
+    def decode(self, start_frame=0, length=None, sink=None, comb=False, comb_sink=None, start_sample=None,
+               stop_sample=None, keep_from=None, firstframe=True, archive=False, init_state=None):
         """Decode frames; sink(frame_u16, pcm_i16, meta) per frame (None: frames stay in HBM).
 
         comb: also run the 2D NTSC comb (comb-ntsc.cxx dim=2) on every frame, in
         order, as one comb process; comb_sink(rgb48) receives each 480x744x3
         frame (None with sink=None: the rgb frames stay in HBM).
+        Field-group sharding (ldgpu/shard.py) hooks: start at start_sample; stop
+        before a frame that would start at or after stop_sample; frames starting
+        before keep_from are decoded (they lock the read / MTF chains) but not
+        output; firstframe: whether the first frame is the capture's first
+        (lddecode.py:90); archive: keep each output field's audio inputs in the
+        field archive instead of computing its 48 kHz audio (the shard's audio
+        time offset is known only after the exchange), see self.shard_frames.
         Returns the number of frames decoded."""
         self.comb, self.comb_sink = comb, comb_sink
+        self.archive, self.arch_next, self.shard_frames = archive, 0, []
+        self.transitions = []
         if comb:
             self.ctx.comb_reset()
         spf = self.rf.samples_per_frame
@@ -507,11 +525,17 @@ class GPUDecoder:
         self.mtf_level, self.audio_offset = 1, 0
         self.last_framenr, self.last_isclv, self.last_read = None, False, None
         self.frame_numbers, self.pcm_samples, self.last_meta = [], 0, None
+        for k, v in (init_state or {}).items():        # chain state handed over by a previous shard
+            setattr(self, k, v)
         nextsample = start_frame * spf if start_sample is None else start_sample
         done = 0
+        nframes_read = 0
         hist = []
         W, H = self.sysp.outlinelen, self.sysp.frame_lines
-        while done < num_frames and self._tell() + bpf * 1.05 <= size:
+        def more(ns):
+            return stop_sample is None or ns < stop_sample
+
+        while done < num_frames and self._tell() + bpf * 1.05 <= size and more(nextsample):
             # nothing known about this capture yet: learn the first fields' parity,
             # VBI and sync positions from a small launch before speculating wide
             # (until P + 2 field starts are known the period extrapolation has nothing to use)
@@ -524,24 +548,30 @@ class GPUDecoder:
             eof = False
             t0 = time.perf_counter()
             self.requested = []
-            while done + len(frames) < num_frames and self._tell() + bpf * 1.05 <= size:
+            while done + len(frames) < num_frames and self._tell() + bpf * 1.05 <= size and more(nextsample):
                 cp = (nextsample, self.mtf_level, self.audio_offset, self.last_framenr, self.last_isclv,
-                      self.last_read)
+                      self.last_read, len(self.transitions), nframes_read)
                 self.field_log = []
                 try:
-                    fr = self.readframe(nextsample, (done + len(frames)) == 0)
+                    fr = self.readframe(nextsample, firstframe and nframes_read == 0)
                 except Miss as m:
                     self._note_miss(m.key)
                     (nextsample, self.mtf_level, self.audio_offset, self.last_framenr, self.last_isclv,
-                     self.last_read) = cp
+                     self.last_read, nt, nframes_read) = cp
+                    del self.transitions[nt:]
                     break
                 if fr is None:
                     eof = True
                     break
+                nframes_read += 1
+                fr.start = nextsample
+                fr.tstart = cp[6]
+                nextsample = fr.nextsample
+                if keep_from is not None and fr.start < keep_from:
+                    continue                    # warm-up frame: chains only
                 fr.fields = [x.record() for x in self.field_log]
                 fr.index = done + len(frames)
                 frames.append(fr)
-                nextsample = fr.nextsample
                 hist = (hist + [x.readsample for x in self.field_log if x.valid])[-16:]
             self.stats['replay_s'] += time.perf_counter() - t0
             self._flush(frames, W, H, sink)
@@ -571,6 +601,18 @@ class GPUDecoder:
                     for r in rgb:
                         self.comb_sink(r)
         af = [(fr_i, x) for fr_i, fr in enumerate(frames) for x in fr.audio_fields]
+        if self.archive:
+            # audio deferred: archive the fields' audio inputs, record the chain positions
+            if af:
+                self.ctx.archive_fields([x.slot for _, x in af], self.arch_next)
+            for i, fr in enumerate(frames):
+                ents = [(self.arch_next + j, x.tidx) for j, (fi, x) in enumerate(af) if fi == i]
+                self.shard_frames.append({'index': fr.index, 'start': int(fr.start), 'tstart': fr.tstart,
+                                          'nextsample': int(fr.nextsample),
+                                          'audio': ents, 'vbi': dict(fr.vbi), 'fields': fr.fields,
+                                          'mtf': float(fr.top.mtf_level)})
+            self.arch_next += len(af)
+            af = []
         if af:
             pcm, counts, _ = self.ctx.field_audio([x.slot for _, x in af], [x.audio_offset for _, x in af])
         per_frame = [[] for _ in frames]

@@ -20,7 +20,8 @@ MAX_VSYNCS = 16
 EXPORTS = ['ldg_create', 'ldg_destroy', 'ldg_last_error', 'ldg_set_filters', 'ldg_set_capture',
            'ldg_decode_reads', 'ldg_field_audio', 'ldg_assemble_frames', 'ldg_debug_read',
            'ldg_comb_ntsc', 'ldg_comb_reset', 'ldg_version', 'ldg_device_count', 'ldg_profile_enable',
-           'ldg_profile_read', 'ldg_synth_capture', 'ldg_capture_download', 'ldg_comb_ntsc_async', 'ldg_sync']
+           'ldg_profile_read', 'ldg_synth_capture', 'ldg_capture_download', 'ldg_comb_ntsc_async', 'ldg_sync',
+           'ldg_archive_fields', 'ldg_archive_audio']
 
 
 class FieldInfo(C.Structure):
@@ -94,6 +95,8 @@ def load(path=LIB_PATH):
     lib.ldg_comb_ntsc.argtypes = [vp, C.c_int, vp, vp, C.c_int]
     lib.ldg_comb_reset.argtypes = [vp]
     lib.ldg_comb_ntsc_async.argtypes = [vp, C.c_int]
+    lib.ldg_archive_fields.argtypes = [vp, C.c_int, vp, C.c_int64]
+    lib.ldg_archive_audio.argtypes = [vp, C.c_int, vp, vp, vp, C.c_int64, vp, vp]
     lib.ldg_sync.argtypes = [vp]
     lib.ldg_profile_enable.argtypes = [vp, C.c_int]
     lib.ldg_profile_read.argtypes = [vp, C.POINTER(KernelStat), C.c_int]
@@ -202,6 +205,23 @@ class Context:
         of = np.ascontiguousarray(offsets, dtype=np.float64)
         self._check(self.lib.ldg_field_audio(self.h, n, _ptr(sl, C.c_int32), _ptr(of), _ptr(pcm, C.c_int16), stride,
                                              _ptr(counts, C.c_int32), _ptr(nxt)), 'ldg_field_audio')
+        return pcm[:n], counts[:n], nxt[:n]
+
+    def archive_fields(self, slots, first):
+        sl = np.ascontiguousarray(slots, dtype=np.int32)
+        self._check(self.lib.ldg_archive_fields(self.h, sl.size, sl.ctypes.data, int(first)), 'ldg_archive_fields')
+
+    def archive_audio(self, entries, offsets):
+        """ldg_field_audio over archive entries -> (pcm[n, 2048], counts, next offsets)."""
+        n = len(entries)
+        stride = 2048
+        pcm = np.zeros((max(n, 1), stride), dtype=np.int16)
+        counts = np.zeros(max(n, 1), dtype=np.int32)
+        nxt = np.zeros(max(n, 1), dtype=np.float64)
+        e = np.ascontiguousarray(entries, dtype=np.int64)
+        o = np.ascontiguousarray(offsets, dtype=np.float64)
+        self._check(self.lib.ldg_archive_audio(self.h, n, e.ctypes.data, o.ctypes.data, pcm.ctypes.data, stride,
+                                               counts.ctypes.data, nxt.ctypes.data), 'ldg_archive_audio')
         return pcm[:n], counts[:n], nxt[:n]
 
     def assemble_frames_device(self, tops, bottoms):

@@ -1,0 +1,180 @@
+"""Field-group sharding of one capture across GPUs.
+
+Fields are independent except for four chains (F10): the read position
+(`nextsample = readsample + nextfieldoffset`), the MTF level from the previous
+CAV frame number, the 48 kHz audio time offset, and the comb's burst-level EMA.
+Each rank decodes a contiguous range of the capture:
+
+1. rank k starts two frames before its boundary B_k and decodes warm-up frames
+   that are not output. The read position is signal-locked: a start converges
+   onto the true chain after one field, and the MTF after one frame. It outputs
+   the frames that start in [B_k, B_{k+1}), with audio deferred: each field's
+   audio inputs go to the device field archive.
+2. One small exchange (all_gather of a per-rank summary):
+   - each rank's first frame start, its last `nextsample` and its end MTF;
+   - the frame count;
+   - the audio-offset transitions (the line count of each frame's last field).
+3. Verification and fix-up:
+   - The chain is exact iff rank k's first frame starts at rank k-1's
+     `nextsample` with rank k-1's end MTF. On a mismatch the rank re-decodes
+     from that boundary state.
+   - The exact audio offset at each rank's start is the offset chain replayed
+     over the transitions of the ranks before it. Each field's 48 kHz audio is
+     then computed from the archive.
+   - Global frame indices are the prefix sum of the frame counts.
+
+The result is identical to a single decode of the whole capture:
+tests/test_shard.py checks it on the GPU, with ranks run one after another, and
+on CPU with gloo for the exchange logic.
+"""
+import numpy as np
+
+
+def audio_next(offset, linecount, line_period):
+    """downscale_audio's returned next offset (lddecode_core.py:432-437, 484)."""
+    frametime = (line_period * linecount) / 1000000
+    gap = 1 / 48000.0
+    ticks = np.arange(offset, frametime + gap, gap, dtype=np.double)
+    return ticks[-1] - frametime
+
+
+def shard_bounds(start, end, spf, world):
+    """Frame-aligned sample boundaries B_0 = start < B_1 < ... < B_world = end."""
+    nfr = max(0, (end - start) // spf)
+    return [start + (nfr * k // world) * spf for k in range(world)] + [end]
+
+
+def replay_offsets(o0, transitions, line_period):
+    """Offsets after each transition, starting from o0: [o0, o1, ..., on]."""
+    out = [o0]
+    for lc in transitions:
+        out.append(audio_next(out[-1], lc, line_period))
+    return out
+
+
+def check_chain(summaries):
+    """Ranks whose first frame does not continue the previous rank's chain (exactly)."""
+    bad = []
+    prev = None
+    for k, s in enumerate(summaries):
+        if s['n'] == 0:
+            continue
+        if prev is not None and (s['first_start'] != prev['last_next'] or s['first_mtf'] != prev['end_mtf']):
+            bad.append(k)
+        prev = s
+    return bad
+
+
+def start_offsets(summaries, line_period):
+    """Exact audio time offset at each rank's first frame (rank 0 starts at 0)."""
+    o, out = 0.0, []
+    for s in summaries:
+        out.append(o)
+        o = replay_offsets(o, s['transitions'], line_period)[-1]
+    return out
+
+
+def frame_offsets(summaries):
+    """Global index of each rank's first frame (exclusive prefix sum of the counts)."""
+    out, acc = [], 0
+    for s in summaries:
+        out.append(acc)
+        acc += s['n']
+    return out
+
+
+class ShardedDecode:
+    """One rank's part of a field-group sharded decode, in two phases."""
+
+    def __init__(self, dec, rank, world, start_frame=0, warmup_frames=2):
+        self.dec, self.rank, self.world = dec, rank, world
+        self.spf = dec.rf.samples_per_frame
+        self.start = start_frame * self.spf
+        self.bounds = shard_bounds(self.start, dec.cap_nsamples, self.spf, world)
+        self.warmup = warmup_frames
+        self.frames = []                    # (frame uint16 or None, local record)
+
+    def _run(self, sink, start_sample, keep_from, firstframe, init=None):
+        dec = self.dec
+        stop = self.bounds[self.rank + 1] if self.rank < self.world - 1 else None
+        self.frames = []
+
+        def keep(pic, audio, meta):
+            self.frames.append(pic)
+            if sink:
+                sink(pic, None, meta)
+
+        dec.decode(start_sample=start_sample, stop_sample=stop, keep_from=keep_from, firstframe=firstframe,
+                   archive=True, sink=keep, init_state=init)
+
+    def local(self, sink=None):
+        """Phase 1: decode this rank's range; returns the summary to exchange."""
+        b = self.bounds[self.rank]
+        if self.rank == 0:
+            self._run(sink, b, None, True)
+        else:
+            self._run(sink, max(0, b - self.warmup * self.spf), b, False)
+        return self.summary()
+
+    def summary(self):
+        dec, sf = self.dec, self.dec.shard_frames
+        t0 = sf[0]['tstart'] if sf else len(dec.transitions)
+        return {'rank': self.rank, 'n': len(sf),
+                'first_start': sf[0]['start'] if sf else None,
+                'first_mtf': sf[0]['mtf'] if sf else None,
+                'last_next': sf[-1]['nextsample'] if sf else None,
+                'end_mtf': float(dec.mtf_level), 'end_framenr': dec.last_framenr, 'end_isclv': dec.last_isclv,
+                'transitions': list(dec.transitions[t0:]), 't0': t0}
+
+    def refix(self, summaries, sink=None):
+        """Re-decode from the previous rank's exact end state (chain mismatch)."""
+        prev = next(s for s in reversed(summaries[:self.rank]) if s['n'])
+        self._run(sink, prev['last_next'], None, False,
+                  init={'mtf_level': prev['end_mtf'], 'last_framenr': prev['end_framenr'],
+                        'last_isclv': prev['end_isclv']})
+        return self.summary()
+
+    def finish(self, summaries):
+        """Phase 2: exact audio from the archive and global frame indices.
+        Returns [(global_index, pcm int16, meta)] for this rank's frames."""
+        dec = self.dec
+        lp = dec.sysp.line_period
+        o0 = start_offsets(summaries, lp)[self.rank]
+        me = summaries[self.rank]
+        offs = replay_offsets(o0, me['transitions'], lp)
+        base = frame_offsets(summaries)[self.rank]
+        ents = [(e, offs[t - me['t0']]) for f in dec.shard_frames for e, t in f['audio']]
+        pcm_by_entry = {}
+        step = dec.capacity
+        for i in range(0, len(ents), step):
+            chunk = ents[i:i + step]
+            pcm, counts, _ = dec.ctx.archive_audio([e for e, _ in chunk], [o for _, o in chunk])
+            for j, (e, _) in enumerate(chunk):
+                if counts[j] < 0:
+                    raise RuntimeError('audio index error (reference: field invalid)')
+                pcm_by_entry[e] = pcm[j, :2 * counts[j]]
+        out = []
+        for i, f in enumerate(dec.shard_frames):
+            parts = [pcm_by_entry[e] for e, _ in f['audio']]
+            audio = np.concatenate(parts) if parts else np.zeros(0, dtype=np.int16)
+            meta = {'frame': base + i, 'vbi': f['vbi'], 'nextsample': f['nextsample'], 'fields': f['fields']}
+            out.append((base + i, audio, meta))
+        return out
+
+
+def decode_sharded(dec, rank, world, allgather, sink=None, start_frame=0):
+    """Run all phases with `allgather(obj) -> [obj per rank]` (torch.distributed
+    all_gather_object, or an in-process stand-in).  Returns this rank's
+    [(global_index, frame, pcm, meta)]."""
+    sd = ShardedDecode(dec, rank, world, start_frame)
+    summ = allgather(sd.local())
+    for _ in range(world):
+        bad = check_chain(summ)
+        if not bad:
+            break
+        mine = sd.refix(summ) if rank in bad else summ[rank]
+        summ = allgather(mine)
+    if check_chain(summ):
+        raise RuntimeError('sharded decode: chain did not converge')
+    res = sd.finish(summ)
+    return [(g, pic, a, m) for (g, a, m), pic in zip(res, sd.frames)]
