@@ -86,9 +86,12 @@ def frame_offsets(summaries):
 class ShardedDecode:
     """One rank's part of a field-group sharded decode, in two phases."""
 
-    def __init__(self, dec, rank, world, start_frame=0, warmup_frames=2):
+    def __init__(self, dec, rank, world, start_frame=0, warmup_frames=2, length=None):
         self.dec, self.rank, self.world = dec, rank, world
         self.spf = dec.rf.samples_per_frame
+        # the whole decode's frame count limit (lddecode.py:49; -l): frames past it are dropped
+        bpf = self.spf * 5 // 4
+        self.limit = length if length is not None else dec.cap_bytes // bpf - start_frame
         self.start = start_frame * self.spf
         self.bounds = shard_bounds(self.start, dec.cap_nsamples, self.spf, world)
         self.warmup = warmup_frames
@@ -155,6 +158,8 @@ class ShardedDecode:
                 pcm_by_entry[e] = pcm[j, :2 * counts[j]]
         out = []
         for i, f in enumerate(dec.shard_frames):
+            if base + i >= self.limit:
+                break
             parts = [pcm_by_entry[e] for e, _ in f['audio']]
             audio = np.concatenate(parts) if parts else np.zeros(0, dtype=np.int16)
             meta = {'frame': base + i, 'vbi': f['vbi'], 'nextsample': f['nextsample'], 'fields': f['fields']}
@@ -162,11 +167,11 @@ class ShardedDecode:
         return out
 
 
-def decode_sharded(dec, rank, world, allgather, sink=None, start_frame=0):
+def decode_sharded(dec, rank, world, allgather, sink=None, start_frame=0, length=None):
     """Run all phases with `allgather(obj) -> [obj per rank]` (torch.distributed
     all_gather_object, or an in-process stand-in).  Returns this rank's
     [(global_index, frame, pcm, meta)]."""
-    sd = ShardedDecode(dec, rank, world, start_frame)
+    sd = ShardedDecode(dec, rank, world, start_frame, length=length)
     summ = allgather(sd.local())
     for _ in range(world):
         bad = check_chain(summ)
