@@ -59,6 +59,18 @@ def main(argv=None):
         print("ERROR: --comb is NTSC only")
         return 1
 
+    world = int(os.environ.get('WORLD_SIZE', '1'))
+    if world > 1:
+        # one process per GPU (python -m torch.distributed.run --nproc-per-node N lddecode.py ...):
+        # field-group sharding of the capture (ldgpu/shard.py); the exchange runs over gloo
+        import torch.distributed as dist
+        dist.init_process_group('gloo')
+        from ldgpu import native
+        ndev = max(1, native.load().ldg_device_count())
+        args.device = int(os.environ.get('LOCAL_RANK', '0')) % ndev
+        if args.comb:
+            print("ERROR: --comb is single-GPU in this build")
+            return 1
     dec = GPUDecoder(system=system, device=args.device, batch=args.batch)
     samples_per_frame = dec.rf.samples_per_frame                 # int(fs / FPS) + 1
     bytes_per_frame = samples_per_frame * 5 // 4                 # for 10-bit packed files
@@ -88,6 +100,8 @@ def main(argv=None):
         return 0
 
     num_frames = req_frames if req_frames is not None else infile_size // bytes_per_frame - firstframe
+    if world > 1:
+        return sharded(args, dec, outname, firstframe, num_frames, nextsample, req_frames)
     tbc = open(outname + '.tbc', 'wb')
     pcm = open(outname + '.pcm', 'wb')
     rgb = open(outname + '.rgb', 'wb') if args.comb else None
@@ -111,6 +125,48 @@ def main(argv=None):
     if not args.no_json:
         with open(outname + '.json', 'w') as fh:
             json.dump(meta_all, fh)
+    return 0
+
+
+def sharded(args, dec, outname, firstframe, num_frames, nextsample, req_frames):
+    """This rank's share of a field-group sharded decode; every rank writes its frames
+    at their global offsets in the .tbc / .pcm, rank 0 writes the .json."""
+    import torch.distributed as dist
+    from ldgpu.shard import decode_sharded
+    rank, world = dist.get_rank(), dist.get_world_size()
+
+    def allgather(obj):
+        out = [None] * world
+        dist.all_gather_object(out, obj)
+        return out
+
+    res = decode_sharded(dec, rank, world, allgather, start_frame=firstframe, length=num_frames,
+                         start_sample=nextsample)
+    sizes = allgather((len(res), sum(a.nbytes for _, _, a, _ in res)))
+    frame_bytes = dec.sysp.outlinelen * dec.sysp.frame_lines * 2
+    first = sum(n for n, _ in sizes[:rank])
+    pcm_off = sum(b for _, b in sizes[:rank])
+    if rank == 0:
+        for ext in ('.tbc', '.pcm'):
+            open(outname + ext, 'wb').close()
+    dist.barrier()
+    with open(outname + '.tbc', 'r+b') as tbc, open(outname + '.pcm', 'r+b') as pcm:
+        tbc.seek(first * frame_bytes)
+        pcm.seek(pcm_off)
+        for g, pic, audio, meta in res:
+            print('frame ', meta['vbi']['framenr'])
+            tbc.write(pic.tobytes())
+            pcm.write(audio.tobytes())
+    metas = allgather([m for _, _, _, m in res])
+    total = sum(n for n, _ in sizes)
+    if rank == 0:
+        if req_frames is not None and total < req_frames:
+            print('Warning: end of file reached before requested number of frames were decoded')
+        if not args.no_json:
+            with open(outname + '.json', 'w') as fh:
+                json.dump([m for part in metas for m in part], fh)
+    dist.barrier()
+    dist.destroy_process_group()
     return 0
 
 

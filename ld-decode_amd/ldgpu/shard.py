@@ -86,13 +86,13 @@ def frame_offsets(summaries):
 class ShardedDecode:
     """One rank's part of a field-group sharded decode, in two phases."""
 
-    def __init__(self, dec, rank, world, start_frame=0, warmup_frames=2, length=None):
+    def __init__(self, dec, rank, world, start_frame=0, warmup_frames=2, length=None, start_sample=None):
         self.dec, self.rank, self.world = dec, rank, world
         self.spf = dec.rf.samples_per_frame
         # the whole decode's frame count limit (lddecode.py:49; -l): frames past it are dropped
         bpf = self.spf * 5 // 4
         self.limit = length if length is not None else dec.cap_bytes // bpf - start_frame
-        self.start = start_frame * self.spf
+        self.start = start_frame * self.spf if start_sample is None else start_sample
         self.bounds = shard_bounds(self.start, dec.cap_nsamples, self.spf, world)
         self.warmup = warmup_frames
         self.frames = []                    # (frame uint16 or None, local record)
@@ -167,11 +167,11 @@ class ShardedDecode:
         return out
 
 
-def decode_sharded(dec, rank, world, allgather, sink=None, start_frame=0, length=None):
+def decode_sharded(dec, rank, world, allgather, sink=None, start_frame=0, length=None, start_sample=None):
     """Run all phases with `allgather(obj) -> [obj per rank]` (torch.distributed
     all_gather_object, or an in-process stand-in).  Returns this rank's
     [(global_index, frame, pcm, meta)]."""
-    sd = ShardedDecode(dec, rank, world, start_frame, length=length)
+    sd = ShardedDecode(dec, rank, world, start_frame, length=length, start_sample=start_sample)
     summ = allgather(sd.local())
     for _ in range(world):
         bad = check_chain(summ)

@@ -99,3 +99,27 @@ def test_cli_seek_and_cut(tmp_path):
     last = dec.findframe(106, first, log=lambda *a: None) + int(spf * .25)
     raw = np.frombuffer(bytes(data), dtype=np.uint8).astype(np.int16)
     assert np.array_equal(r16, raw[first:last])
+
+
+@pytest.mark.gpu
+def test_cli_sharded_two_ranks_equal_single(tmp_path):
+    """torch.distributed.run with 2 ranks (field-group sharding) writes the same
+    .tbc / .pcm / .json as the single-process CLI."""
+    import socket
+    from ldgpu.synth import make_capture
+    data = make_capture(int(40e6 * 0.6), 'u8', first_frame=500, seed=13)
+    cap = tmp_path / 'cap.u8'
+    cap.write_bytes(bytes(data))
+    r = run_cli(cap, tmp_path / 'one')
+    assert r.returncode == 0, r.stderr[-2000:]
+    with socket.socket() as sk:
+        sk.bind(('127.0.0.1', 0))
+        port = sk.getsockname()[1]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY='0')
+    r = subprocess.run([sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', '--nproc-per-node', '2',
+                        '--master-addr', '127.0.0.1', '--master-port', str(port), CLI, str(cap),
+                        str(tmp_path / 'two')], capture_output=True, text=True, timeout=600, env=env)
+    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-3000:])
+    for ext in ('.tbc', '.pcm'):
+        assert (tmp_path / ('one' + ext)).read_bytes() == (tmp_path / ('two' + ext)).read_bytes(), ext
+    assert json.load(open(tmp_path / 'one.json')) == json.load(open(tmp_path / 'two.json'))
