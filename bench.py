@@ -181,6 +181,7 @@ def main():
         'checks': {'cav_framenr_consecutive': consecutive, 'synth_s': round(synth_s, 2),
                    'reads_decoded': dec.stats['reads'], 'reads_used': dec.stats['reads_used'],
                    'batches': dec.stats['batches'], 'misses': dec.stats.get('misses', 0),
+                   'host_s': {k: round(dec.stats.get(k, 0.0), 4) for k in ('plan_s', 'gpu_s', 'replay_s', 'flush_s')},
                    'miss_sample': dec.stats.get('miss_log', [])[:12]},
     }
     print(json.dumps(line), flush=True)

@@ -145,6 +145,7 @@ class GPUDecoder:
         self.field_nom = int(round(self.rf.freq_hz / self.sysp.fps / 2))
         self.trace = None          # diagnostics: planner steps (tools/miss_probe.py)
         self.comb, self.comb_sink = False, None
+        self.pending = None                # (keys, slots) of the outstanding decode launch
         self.transitions = []              # audio-offset chain: linecount of each transition's field
         self.archive, self.arch_next, self.shard_frames = False, 0, []
 
@@ -300,8 +301,14 @@ class GPUDecoder:
         return new, chain
 
     def _launch(self, keys, protect):
-        """Decode `keys` into free slots, evicting least-recently-used cache entries
-        not in `protect` (the reads the replay is about to consume) as needed."""
+        """Decode `keys` now (launch and wait)."""
+        self._launch_async(keys, protect)
+        self._launch_wait()
+
+    def _launch_async(self, keys, protect):
+        """Start decoding `keys` into free slots, evicting least-recently-used cache
+        entries not in `protect` (the reads the replay is about to consume) as
+        needed; _launch_wait() adds the records to the cache."""
         used = {v[0] for v in self.cache.values()}
         free = [s for s in range(self.capacity) if s not in used]
         if len(free) < len(keys):
@@ -312,10 +319,20 @@ class GPUDecoder:
             raise RuntimeError('read cache full (capacity %d)' % self.capacity)
         slots = free[:len(keys)]
         t0 = time.perf_counter()
-        infos = self.ctx.decode_reads([k[0] for k in keys], [k[1] for k in keys], slots)
+        self.ctx.decode_reads_async([k[0] for k in keys], [k[1] for k in keys], slots)
         self.stats['gpu_s'] += time.perf_counter() - t0
         self.stats['batches'] += 1
         self.stats['reads'] += len(keys)
+        self.pending = (keys, slots)
+
+    def _launch_wait(self):
+        if self.pending is None:
+            return
+        keys, slots = self.pending
+        t0 = time.perf_counter()
+        infos = self.ctx.decode_reads_wait()
+        self.stats['wait_s'] = self.stats.get('wait_s', 0.0) + time.perf_counter() - t0
+        self.pending = None
         import bisect
         for k, sl, inf in zip(keys, slots, infos):
             self.cache[k] = (sl, inf)
@@ -540,10 +557,16 @@ class GPUDecoder:
             # VBI and sync positions from a small launch before speculating wide
             # (until P + 2 field starts are known the period extrapolation has nothing to use)
             want = self.batch if len(hist) >= self.period + 2 else min(self.batch, 8 if self._hint_keys else 4)
+            tp = time.perf_counter()
             plan, chain = self._plan(nextsample, self.mtf_level, self.last_framenr, self.last_isclv, done == 0,
                                      want, hist)
+            self.stats['plan_s'] = self.stats.get('plan_s', 0.0) + time.perf_counter() - tp
             if plan:
-                self._launch(plan, set(chain))
+                # decode the reads beyond the cached path while the host replays
+                # and outputs that path (the replay stops at the first pending read)
+                self._launch_async(plan, set(chain))
+                if not chain:
+                    self._launch_wait()
             frames = []
             eof = False
             t0 = time.perf_counter()
@@ -574,11 +597,15 @@ class GPUDecoder:
                 frames.append(fr)
                 hist = (hist + [x.readsample for x in self.field_log if x.valid])[-16:]
             self.stats['replay_s'] += time.perf_counter() - t0
+            tf = time.perf_counter()
             self._flush(frames, W, H, sink)
+            self.stats['flush_s'] = self.stats.get('flush_s', 0.0) + time.perf_counter() - tf
+            self._launch_wait()
             done += len(frames)
             self.stats['reads_used'] += sum(len(f.fields) for f in frames)
             if eof or (not frames and not plan):
                 break
+        self._launch_wait()
         self.ctx.sync()
         return done
 

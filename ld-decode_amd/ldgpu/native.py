@@ -21,7 +21,7 @@ EXPORTS = ['ldg_create', 'ldg_destroy', 'ldg_last_error', 'ldg_set_filters', 'ld
            'ldg_decode_reads', 'ldg_field_audio', 'ldg_assemble_frames', 'ldg_debug_read',
            'ldg_comb_ntsc', 'ldg_comb_reset', 'ldg_version', 'ldg_device_count', 'ldg_profile_enable',
            'ldg_profile_read', 'ldg_synth_capture', 'ldg_capture_download', 'ldg_comb_ntsc_async', 'ldg_sync',
-           'ldg_archive_fields', 'ldg_archive_audio']
+           'ldg_archive_fields', 'ldg_archive_audio', 'ldg_decode_reads_async', 'ldg_decode_reads_wait']
 
 
 class FieldInfo(C.Structure):
@@ -95,6 +95,8 @@ def load(path=LIB_PATH):
     lib.ldg_comb_ntsc.argtypes = [vp, C.c_int, vp, vp, C.c_int]
     lib.ldg_comb_reset.argtypes = [vp]
     lib.ldg_comb_ntsc_async.argtypes = [vp, C.c_int]
+    lib.ldg_decode_reads_async.argtypes = [vp, C.c_int, vp, vp, vp]
+    lib.ldg_decode_reads_wait.argtypes = [vp, vp]
     lib.ldg_archive_fields.argtypes = [vp, C.c_int, vp, C.c_int64]
     lib.ldg_archive_audio.argtypes = [vp, C.c_int, vp, vp, vp, C.c_int64, vp, vp]
     lib.ldg_sync.argtypes = [vp]
@@ -193,6 +195,21 @@ class Context:
         info = (FieldInfo * n)()
         self._check(self.lib.ldg_decode_reads(self.h, n, _ptr(s, C.c_int64), _ptr(m), _ptr(sl, C.c_int32), info),
                     'ldg_decode_reads')
+        return list(info)
+
+    def decode_reads_async(self, starts, mtfs, slots):
+        """Launch a decode (ldg_decode_reads_async); decode_reads_wait() returns its records."""
+        self._pending = (np.ascontiguousarray(starts, dtype=np.int64), np.ascontiguousarray(mtfs, dtype=np.float64),
+                         np.ascontiguousarray(slots, dtype=np.int32))
+        s, m, sl = self._pending
+        self._check(self.lib.ldg_decode_reads_async(self.h, s.size, s.ctypes.data, m.ctypes.data, sl.ctypes.data),
+                    'ldg_decode_reads_async')
+
+    def decode_reads_wait(self):
+        n = self._pending[0].size
+        info = (FieldInfo * n)()
+        self._check(self.lib.ldg_decode_reads_wait(self.h, info), 'ldg_decode_reads_wait')
+        self._pending = None
         return list(info)
 
     def field_audio(self, slots, offsets):
