@@ -15,7 +15,7 @@
 // C2R  = 9 (NTSC) / 10 (PAL); plus 2 x 1024-point audio IFFTs.
 #include <hip/hip_runtime.h>
 #include "common.hpp"
-#include "fft.hpp"
+#include "fft8k.hpp"
 
 using namespace ldg;
 
@@ -70,75 +70,98 @@ __device__ __forceinline__ double fold_tau(double d) {
   return d < 0.0 ? d + TAU : d;
 }
 
-// Half-spectrum bins k in [0, M/2] paired with M-k: thread tid owns
-// k = tid + 1024 q (q < 4) and, thread 0 only, k = M/2 (slot 4).
-struct Pairs {
-  double2 a[5], b[5];   // value at k and at M-k of each pair slot
+// Half-spectrum pair slots over the digit-reversed spectrum layout that
+// fft8k_dif produces (fft8k.hpp): thread tid owns slots c = 0..3 and thread 0
+// also slot 4, 4097 slots covering the bins k in [0, M] as pairs (k, M-k).
+// Slot c < 3 (and c == 3 for tid < 512) takes sub-array q = 1..7 position
+// 512 q + j, whose partner M-k sits at 512 (16-q) + 511 - j: contiguous (and
+// reversed) across lanes.  The rest pair up sub-array 8 with itself and
+// sub-array 0 (k = 16 k', a 512-point digit-reversed array) with itself.
+//   p, pp: LDS positions of k and of M-k (pp == p for k = 0, whose partner is
+//   the Nyquist bin M, and for k = M/2); gp: table index of M-k (M for k = 0).
+struct Slot {
+  int p, pp, gp;
 };
+
+__device__ __forceinline__ Slot slot_of(int tid, int c) {
+  if (c < 3 || (c == 3 && tid < 512)) {
+    const int i = tid + 1024 * c, q = 1 + (i >> 9), j = i & 511;
+    const int pp = 512 * (16 - q) + 511 - j;
+    return {512 * q + j, pp, pp};
+  }
+  if (c == 3 && tid < 768) {
+    const int j = tid - 512;
+    return {4096 + j, 4607 - j, 4607 - j};
+  }
+  const int z = c == 4 ? 256 : tid - 768;
+  int p, pp;
+  if (z < 192) {
+    const int sb = 1 + (z >> 6), jj = z & 63;
+    p = 64 * sb + jj;
+    pp = 64 * (8 - sb) + 63 - jj;
+  } else if (z < 224) {
+    p = 256 + (z - 192);
+    pp = 319 - (z - 192);
+  } else if (z < 248) {
+    const int w = z - 224, u = 1 + (w >> 3), v = w & 7;
+    p = 8 * u + v;
+    pp = 8 * (8 - u) + 7 - v;
+  } else if (z < 252) {
+    p = 32 + (z - 248);
+    pp = 39 - (z - 248);
+  } else if (z < 255) {
+    p = z - 251;
+    pp = 8 - p;
+  } else if (z == 255) {
+    return {0, 0, M};
+  } else {
+    return {4, 4, 4};
+  }
+  return {p, pp, pp};
+}
 
 // Opaque copy of tid: stops the compiler from hoisting per-lane twiddle loads
 // and addresses that repeat across the kernel's transforms (and spilling them).
 __device__ __forceinline__ int fresh(int tid) { asm volatile("" : "+v"(tid)); return tid; }
 
-__device__ __forceinline__ int pair_k(int tid, int q) { return q < 4 ? tid + 1024 * q : 4096; }
-__device__ __forceinline__ bool pair_live(int tid, int q) { return q < 4 || tid == 0; }
+__device__ __forceinline__ bool pair_live(int tid, int c) { return c < 4 || tid == 0; }
 
-// Half-spectrum of the real signal currently transformed in LDS, for my pairs.
-__device__ __forceinline__ void split_pairs(CBuf x, const double2* __restrict__ tw, int tid, Pairs& X) {
+// W_2M^(M-k) = -conj(W_2M^k)
+__device__ __forceinline__ double2 tw_mirror(double2 w) { return make_double2(-w.x, w.y); }
+
+struct Pairs {
+  double2 a[5], b[5];   // value at k and at M-k of each pair slot
+};
+
+// Half-spectrum of the real signal just transformed by fft8k_dif, for my slots.
+// twk[p] = W_2M^(dr_nat(p)).
+__device__ __forceinline__ void split_pairs(const CBuf x, const double2* __restrict__ twk, int tid, Pairs& X) {
   tid = fresh(tid);
 #pragma unroll
-  for (int q = 0; q < 5; q++) {
-    if (!pair_live(tid, q)) continue;
-    const int k = pair_k(tid, q), kp = M - k;
-    const double2 A = x[k];
-    const double2 B = x[kp & (M - 1)];
-    X.a[q] = rsplit(A, B, tw[k]);
-    X.b[q] = rsplit(B, A, tw[kp]);
+  for (int c = 0; c < 5; c++) {
+    if (!pair_live(tid, c)) continue;
+    const Slot sl = slot_of(tid, c);
+    const double2 A = x[sl.p], B = x[sl.pp];
+    const double2 wk = twk[sl.p];
+    X.a[c] = rsplit(A, B, wk);
+    X.b[c] = rsplit(B, A, tw_mirror(wk));
   }
 }
 
-// Write merge(D * G) for my pairs (registers) into LDS (input of a C2R inverse FFT).
-__device__ __forceinline__ void merge_pairs(CBuf x, const double2* __restrict__ tw, const double2* __restrict__ G,
-                                            int tid, const Pairs& D) {
+// Write merge(D * G) for my slots into LDS, digit-reversed (input of fft8k_dit).
+// G: a filter in digit-reversed order (G[p] = filter[dr_nat(p)], G[M] = filter[M]).
+__device__ __forceinline__ void merge_pairs(const CBuf x, const double2* __restrict__ twk,
+                                            const double2* __restrict__ G, int tid, const Pairs& D) {
   tid = fresh(tid);
 #pragma unroll
-  for (int q = 0; q < 5; q++) {
-    if (!pair_live(tid, q)) continue;
-    const int k = pair_k(tid, q), kp = M - k;
-    const double2 Pk = cmul(D.a[q], G[k]);
-    const double2 Pkp = cmul(D.b[q], G[kp]);
-    x[k] = cmerge(Pk, Pkp, tw[k]);
-    if (kp < M && kp != k) x[kp] = cmerge(Pkp, Pk, tw[kp]);
-  }
-}
-
-// Split the real-signal spectrum in LDS and park my pairs in global memory
-// (slot 2q: bin k, slot 2q+1: bin M-k; coalesced, this lane's own entries).
-__device__ __forceinline__ void park_split(CBuf x, const double2* __restrict__ tw, int tid, double2* __restrict__ park) {
-  tid = fresh(tid);
-#pragma unroll
-  for (int q = 0; q < 5; q++) {
-    if (!pair_live(tid, q)) continue;
-    const int k = pair_k(tid, q), kp = M - k;
-    const double2 A = x[k];
-    const double2 B = x[kp & (M - 1)];
-    park[(2 * q) * T] = rsplit(A, B, tw[k]);
-    park[(2 * q + 1) * T] = rsplit(B, A, tw[kp]);
-  }
-}
-
-// Write merge(D * G) for my parked pairs into LDS (input of a C2R inverse FFT).
-__device__ __forceinline__ void merge_filtered(CBuf x, const double2* __restrict__ tw, const double2* __restrict__ G,
-                                               int tid, const double2* __restrict__ park) {
-  tid = fresh(tid);
-#pragma unroll
-  for (int q = 0; q < 5; q++) {
-    if (!pair_live(tid, q)) continue;
-    const int k = pair_k(tid, q), kp = M - k;
-    const double2 Pk = cmul(park[(2 * q) * T], G[k]);
-    const double2 Pkp = cmul(park[(2 * q + 1) * T], G[kp]);
-    x[k] = cmerge(Pk, Pkp, tw[k]);
-    if (kp < M && kp != k) x[kp] = cmerge(Pkp, Pk, tw[kp]);
+  for (int c = 0; c < 5; c++) {
+    if (!pair_live(tid, c)) continue;
+    const Slot sl = slot_of(tid, c);
+    const double2 wk = twk[sl.p];
+    const double2 Pk = cmul(D.a[c], G[sl.p]);
+    const double2 Pkp = cmul(D.b[c], G[sl.gp]);
+    x[sl.p] = cmerge(Pk, Pkp, wk);
+    if (sl.pp != sl.p) x[sl.pp] = cmerge(Pkp, Pk, tw_mirror(wk));
   }
 }
 
@@ -149,7 +172,7 @@ __device__ __forceinline__ void merge_filtered(CBuf x, const double2* __restrict
 // parked there, coalesced, while the even half is transformed).
 extern "C" __global__ __launch_bounds__(1024) void ldg_k_demod(
     const int32_t* __restrict__ smap, const ReadDesc* __restrict__ reads, const uint8_t* __restrict__ cap, int64_t cap_first, int64_t cap_nsamp,
-    int fmt, const double2* __restrict__ tw, const double2* __restrict__ rf_filt,
+    int fmt, const double2* __restrict__ tw, const double2* __restrict__ twk, const double2* __restrict__ rf_filt,
     const double2* __restrict__ g_video, const double2* __restrict__ g_05, const double2* __restrict__ g_burst,
     const double2* __restrict__ g_pilot, const double2* __restrict__ g_psync,
     const double2* __restrict__ a_lfilt, const double2* __restrict__ a_rfilt, SysConst C,
@@ -184,45 +207,53 @@ extern "C" __global__ __launch_bounds__(1024) void ldg_k_demod(
     const int m = tid + T * q;
     X_[m] = make_double2(load_sample(cap, fmt, rel0 + 2 * m), load_sample(cap, fmt, rel0 + 2 * m + 1));
   }
-  fft_lds<M, T, false>(X_, tw, tid);
+  fft8k_dif<false>(s_x, tw, tid);
 
   // ---- 2. analytic-signal spectra and the audio carrier slices ---------------
   // Y = X * RFVideo*MTF^m; the 16384-point IFFT of Y is done as its even/odd
   // (radix-2 DIF) halves: even half -> LDS, odd half -> ospill.  The audio
   // slices (lddecode_core.py:321-328, audio_fdslice lo [a0,a0+512), hi
   // mirrored) go to the separate 32 KiB audio buffer.  X dies here.
+  // Spectra are digit-reversed here (fft8k.hpp); F and the filters are stored
+  // in the same order (F[p] = bin dr_nat(p), F[M + p] = bin M + dr_nat(p)).
   {
     Pairs X;
-    split_pairs(X_, tw, tid, X);
+    split_pairs(X_, twk, tid, X);
     __syncthreads();
     const int a0 = C.audio_lo0;
+    const int t = fresh(tid);
 #pragma unroll
-    for (int q = 0; q < 5; q++) {
-      if (!pair_live(tid, q)) continue;
-      const int k = pair_k(tid, q), kp = M - k;
-      if (q < 4) {
-        const double2 xk = X.a[q];
-        if (k >= a0 && k < a0 + 512) {
-          const int j = k - a0;
+    for (int c = 0; c < 5; c++) {
+      if (!pair_live(t, c)) continue;
+      const Slot sl = slot_of(t, c);
+      const int k = dr_nat(sl.p), kp = M - k;
+      // audio carrier slices from the bins k and M-k of this slot
+#pragma unroll
+      for (int e = 0; e < 2; e++) {
+        const int kk = e ? kp : k;
+        const double2 xk = e ? X.b[c] : X.a[c];
+        if (kk >= a0 && kk < a0 + 512) {
+          const int j = kk - a0;
           A_[j] = cmul(xk, a_lfilt[j]);            // left at [0,1024), right at [1024,2048)
           A_[1024 + j] = cmul(xk, a_rfilt[j]);
         }
-        if (k > a0 && k <= a0 + 512) {
-          const int j = a0 + 1024 - k;
+        if (kk > a0 && kk <= a0 + 512) {
+          const int j = a0 + 1024 - kk;
           const double2 xc = conj2(xk);
           A_[j] = cmul(xc, a_lfilt[j]);
           A_[1024 + j] = cmul(xc, a_rfilt[j]);
         }
       }
-      const double2 yk = cmul(X.a[q], F[k]);
-      const double2 yk2 = cmul(conj2(X.b[q]), F[k + M]);
-      X_[k] = cadd(yk, yk2);
-      osp[(2 * q) * T] = cmulc(csub(yk, yk2), tw[k]);
-      if (kp < M && kp != k) {
-        const double2 ykp = cmul(X.b[q], F[kp]);
-        const double2 ykp2 = cmul(conj2(X.a[q]), F[kp + M]);
-        X_[kp] = cadd(ykp, ykp2);
-        osp[(2 * q + 1) * T] = cmulc(csub(ykp, ykp2), tw[kp]);
+      const double2 wk = twk[sl.p];
+      const double2 yk = cmul(X.a[c], F[sl.p]);
+      const double2 yk2 = cmul(conj2(X.b[c]), F[M + sl.p]);
+      X_[sl.p] = cadd(yk, yk2);
+      osp[(2 * c) * T] = cmulc(csub(yk, yk2), wk);
+      if (sl.pp != sl.p) {
+        const double2 ykp = cmul(X.b[c], F[sl.pp]);
+        const double2 ykp2 = cmul(conj2(X.a[c]), F[M + sl.pp]);
+        X_[sl.pp] = cadd(ykp, ykp2);
+        osp[(2 * c + 1) * T] = cmulc(csub(ykp, ykp2), tw_mirror(wk));
       }
     }
   }
@@ -259,19 +290,22 @@ extern "C" __global__ __launch_bounds__(1024) void ldg_k_demod(
   }
 
   // ---- 4. analytic IFFTs (even, odd) -> instantaneous phase --------------------
-  fft_lds<M, T, true>(X_, tw, tid);
+  fft8k_dit<true>(s_x, tw, tid);
   double the[8], tho[8];
 #pragma unroll
   for (int q = 0; q < 8; q++) { const double2 z = X_[tid + T * q]; the[q] = atan2(z.y, z.x); }
   __syncthreads();
+  {
+    const int t = fresh(tid);
 #pragma unroll
-  for (int q = 0; q < 5; q++) {
-    if (!pair_live(tid, q)) continue;
-    const int k = pair_k(tid, q), kp = M - k;
-    X_[k] = osp[(2 * q) * T];
-    if (kp < M && kp != k) X_[kp] = osp[(2 * q + 1) * T];
+    for (int c = 0; c < 5; c++) {
+      if (!pair_live(t, c)) continue;
+      const Slot sl = slot_of(t, c);
+      X_[sl.p] = osp[(2 * c) * T];
+      if (sl.pp != sl.p) X_[sl.pp] = osp[(2 * c + 1) * T];
+    }
   }
-  fft_lds<M, T, true>(X_, tw, tid);
+  fft8k_dit<true>(s_x, tw, tid);
 #pragma unroll
   for (int q = 0; q < 8; q++) { const double2 z = X_[tid + T * q]; tho[q] = atan2(z.y, z.x); }
   __syncthreads();
@@ -295,15 +329,15 @@ extern "C" __global__ __launch_bounds__(1024) void ldg_k_demod(
 #pragma unroll
     for (int q = 0; q < 8; q++) X_[tid + T * q] = make_double2(d0[q], d1[q]);
   }
-  fft_lds<M, T, false>(X_, tw, tid);
+  fft8k_dif<false>(s_x, tw, tid);
   Pairs D;
-  split_pairs(X_, tw, tid, D);
+  split_pairs(X_, twk, tid, D);
   __syncthreads();
 
   const double inv = 1.0 / (double)M;
   auto emit = [&](int ch, const double2* G) {
-    merge_pairs(X_, tw, G, tid, D);
-    fft_lds<M, T, true>(X_, tw, tid);
+    merge_pairs(X_, twk, G, tid, D);
+    fft8k_dit<true>(s_x, tw, tid);
     double* o = vout + (int64_t)ch * vchan_stride;
     const int t = fresh(tid);
 #pragma unroll
@@ -321,8 +355,8 @@ extern "C" __global__ __launch_bounds__(1024) void ldg_k_demod(
   if (C.n_chan > 4) emit(CH_PILOT, g_pilot);
 
   // ---- 6. 0.5 MHz channel (rolled by -F05_offset) and the sync detector --------
-  merge_pairs(X_, tw, g_05, tid, D);
-  fft_lds<M, T, true>(X_, tw, tid);
+  merge_pairs(X_, twk, g_05, tid, D);
+  fft8k_dit<true>(s_x, tw, tid);
   {
     double v0[8], v1[8];
 #pragma unroll
@@ -344,8 +378,8 @@ extern "C" __global__ __launch_bounds__(1024) void ldg_k_demod(
                             (v1[q] >= C.sync_lo && v1[q] <= C.sync_hi) ? 1.0 : 0.0);
     }
   }
-  fft_lds<M, T, false>(X_, tw, tid);
-  split_pairs(X_, tw, tid, D);
+  fft8k_dif<false>(s_x, tw, tid);
+  split_pairs(X_, twk, tid, D);
   __syncthreads();
   emit(CH_SYNC, g_psync);
 }
@@ -435,14 +469,20 @@ extern "C" __global__ __launch_bounds__(1024) void ldg_k_audio2(
 extern "C" __global__ void ldg_k_rf_table(const double2* __restrict__ rfvideo, const double2* __restrict__ mtf,
                                            const double* __restrict__ mtf_logabs, const double* __restrict__ mtf_arg,
                                            const double* __restrict__ mtfs, double2* __restrict__ tables) {
-  // grid: (BLOCKLEN / 256, n_tables); table y has mtf level mtfs[y]
-  const int k = blockIdx.x * blockDim.x + threadIdx.x;
-  if (k >= BLOCKLEN) return;
+  // grid: (BLOCKLEN / 256, n_tables); table y has mtf level mtfs[y].  Entry o
+  // holds bin dr_nat(o) (o < M) or M + dr_nat(o - M): the order of the demod's
+  // digit-reversed spectra.
+  const int o = blockIdx.x * blockDim.x + threadIdx.x;
+  if (o >= BLOCKLEN) return;
+  const int k = o < M ? dr_nat(o) : M + dr_nat(o - M);
   const double m = mtfs[blockIdx.y];
   double2* out = tables + (size_t)blockIdx.y * BLOCKLEN;
   const double2 r = rfvideo[k];
   double2 p;
-  if (m == 0.0) { out[k] = r; return; }
+  if (m == 0.0) {
+    out[o] = r;
+    return;
+  }
   if (m == 1.0) p = mtf[k];
   else {
     const double mag = exp(m * mtf_logabs[k]);
@@ -450,5 +490,5 @@ extern "C" __global__ void ldg_k_rf_table(const double2* __restrict__ rfvideo, c
     sincos(m * mtf_arg[k], &s, &c);
     p = make_double2(mag * c, mag * s);
   }
-  out[k] = cmul(r, p);
+  out[o] = cmul(r, p);
 }
