@@ -28,6 +28,15 @@ def up_to_date():
     return all(os.path.getmtime(s) <= t for s in sources())
 
 
+def build_variant(out, defines=(), verbose=True):
+    """A profiling build (e.g. defines=('LDG_STAMPS',)) at another path; load it with LDGPU_LIB."""
+    cmd = [HIPCC] + FLAGS + ['-D' + d for d in defines] + [os.path.join(CSRC, 'ldgpu.hip'), '-o', out]
+    if verbose:
+        print(' '.join(cmd), flush=True)
+    subprocess.run(cmd, check=True, cwd=CSRC)
+    return out
+
+
 def build(force=False, verbose=True):
     if not force and up_to_date():
         if verbose:

@@ -167,6 +167,24 @@ __device__ __forceinline__ void merge_pairs(const CBuf x, const double2* __restr
 
 }  // namespace
 
+// In-kernel phase stamps (profiling builds only: -DLDG_STAMPS, tools/demod_stamps.py):
+// thread 0 of the first LDG_STAMP_BLOCKS workgroups records the shader clock
+// at each phase boundary.
+#ifdef LDG_STAMPS
+constexpr int LDG_STAMP_BLOCKS = 8192;
+__device__ unsigned long long g_stamps[LDG_STAMP_BLOCKS][32];
+#define STAMP(i)                                                                   \
+  do {                                                                             \
+    __syncthreads();                                                               \
+    if (threadIdx.x == 0 && blockIdx.x < LDG_STAMP_BLOCKS)                         \
+      g_stamps[blockIdx.x][i] = __builtin_readcyclecounter();                      \
+  } while (0)
+#else
+#define STAMP(i) \
+  do {           \
+  } while (0)
+#endif
+
 // grid: n_reads * MAX_BLOCKS_PER_READ workgroups of 1024 threads.
 // ospill: 10 x 1024 double2 per workgroup (the odd-half analytic spectrum is
 // parked there, coalesced, while the even half is transformed).
@@ -183,6 +201,7 @@ extern "C" __global__ __launch_bounds__(1024) void ldg_k_demod(
   __shared__ double2 s_a[2048];       // 32 KiB: the two 1024-point audio transforms
   const CBuf X_{s_x}, A_{s_a};
   const int tid = threadIdx.x;
+  STAMP(0);
   const int slot = smap[blockIdx.x / MAX_BLOCKS_PER_READ];
   const int b = blockIdx.x % MAX_BLOCKS_PER_READ;
   const ReadDesc rd = reads[slot];
@@ -202,12 +221,35 @@ extern "C" __global__ __launch_bounds__(1024) void ldg_k_demod(
   constexpr double TAU = 6.283185307179586;
 
   // ---- 1. raw samples -> z[m] = x[2m] + i x[2m+1]; forward FFT ---------------
+  if (fmt == 0 || fmt == 1) {
+    // thread t takes samples [16 t, 16 t + 16) with 16-byte loads (unaligned
+    // global access): z[8 t + r] = (x[16 t + 2 r], x[16 t + 2 r + 1])
+    double x[16];
+    if (fmt == 0) {
+      uint4 w;
+      __builtin_memcpy(&w, cap + rel0 + 16 * tid, 16);
+      const uint32_t wd[4] = {w.x, w.y, w.z, w.w};
 #pragma unroll
-  for (int q = 0; q < 8; q++) {
-    const int m = tid + T * q;
-    X_[m] = make_double2(load_sample(cap, fmt, rel0 + 2 * m), load_sample(cap, fmt, rel0 + 2 * m + 1));
+      for (int i = 0; i < 16; i++) x[i] = (double)((wd[i >> 2] >> (8 * (i & 3))) & 0xffu);
+    } else {
+      uint4 w[2];
+      __builtin_memcpy(w, reinterpret_cast<const int16_t*>(cap) + rel0 + 16 * tid, 32);
+      const uint32_t wd[8] = {w[0].x, w[0].y, w[0].z, w[0].w, w[1].x, w[1].y, w[1].z, w[1].w};
+#pragma unroll
+      for (int i = 0; i < 16; i++) x[i] = (double)(int16_t)(wd[i >> 1] >> (16 * (i & 1)));
+    }
+#pragma unroll
+    for (int r = 0; r < 8; r++) X_[8 * tid + r] = make_double2(x[2 * r], x[2 * r + 1]);
+  } else {
+#pragma unroll
+    for (int q = 0; q < 8; q++) {
+      const int m = tid + T * q;
+      X_[m] = make_double2(load_sample(cap, fmt, rel0 + 2 * m), load_sample(cap, fmt, rel0 + 2 * m + 1));
+    }
   }
+  STAMP(1);
   fft8k_dif<false>(s_x, tw, tid);
+  STAMP(2);
 
   // ---- 2. analytic-signal spectra and the audio carrier slices ---------------
   // Y = X * RFVideo*MTF^m; the 16384-point IFFT of Y is done as its even/odd
@@ -219,31 +261,27 @@ extern "C" __global__ __launch_bounds__(1024) void ldg_k_demod(
   {
     Pairs X;
     split_pairs(X_, twk, tid, X);
+    {
+      // audio carrier slices (lddecode_core.py:321-328): thread t < 512 takes
+      // bin k = a0 + t into slot j = t; thread t >= 512 the mirrored bin
+      // k = a0 + 1 + (t - 512), conjugated, into slot j = a0 + 1024 - k
+      const int t = fresh(tid);
+      const int a0 = C.audio_lo0;
+      const bool mir = t >= 512;
+      const int k = mir ? a0 + 1 + (t - 512) : a0 + t;
+      const int j = mir ? a0 + 1024 - k : t;
+      double2 xk = rsplit(X_[dr_pos(k)], X_[dr_pos(M - k)], tw[k]);
+      if (mir) xk = conj2(xk);
+      const double2 al = cmul(xk, a_lfilt[j]), ar = cmul(xk, a_rfilt[j]);
+      A_[j] = al;                       // left at [0,1024), right at [1024,2048)
+      A_[1024 + j] = ar;
+    }
     __syncthreads();
-    const int a0 = C.audio_lo0;
     const int t = fresh(tid);
 #pragma unroll
     for (int c = 0; c < 5; c++) {
       if (!pair_live(t, c)) continue;
       const Slot sl = slot_of(t, c);
-      const int k = dr_nat(sl.p), kp = M - k;
-      // audio carrier slices from the bins k and M-k of this slot
-#pragma unroll
-      for (int e = 0; e < 2; e++) {
-        const int kk = e ? kp : k;
-        const double2 xk = e ? X.b[c] : X.a[c];
-        if (kk >= a0 && kk < a0 + 512) {
-          const int j = kk - a0;
-          A_[j] = cmul(xk, a_lfilt[j]);            // left at [0,1024), right at [1024,2048)
-          A_[1024 + j] = cmul(xk, a_rfilt[j]);
-        }
-        if (kk > a0 && kk <= a0 + 512) {
-          const int j = a0 + 1024 - kk;
-          const double2 xc = conj2(xk);
-          A_[j] = cmul(xc, a_lfilt[j]);
-          A_[1024 + j] = cmul(xc, a_rfilt[j]);
-        }
-      }
       const double2 wk = twk[sl.p];
       const double2 yk = cmul(X.a[c], F[sl.p]);
       const double2 yk2 = cmul(conj2(X.b[c]), F[M + sl.p]);
@@ -258,6 +296,7 @@ extern "C" __global__ __launch_bounds__(1024) void ldg_k_demod(
     }
   }
 
+  STAMP(3);
   // ---- 3. audio phase 1: 2 x IFFT1024 -> FM demod (lddecode_core.py:321-328) ----
   {
     const int g = tid >> 9, lt = tid & 511;
@@ -289,31 +328,41 @@ extern "C" __global__ __launch_bounds__(1024) void ldg_k_demod(
     }
   }
 
+  STAMP(4);
   // ---- 4. analytic IFFTs (even, odd) -> instantaneous phase --------------------
-  fft8k_dit<true>(s_x, tw, tid);
+  // One loop body for both halves: one copy of the inverse FFT in the code (the
+  // kernel would outgrow the instruction cache with every transform inlined).
   double the[8], tho[8];
+#pragma clang loop unroll(disable)
+  for (int h = 0; h < 2; h++) {
+    if (h) {
+      const int t = fresh(tid);
 #pragma unroll
-  for (int q = 0; q < 8; q++) { const double2 z = X_[tid + T * q]; the[q] = atan2(z.y, z.x); }
-  __syncthreads();
-  {
-    const int t = fresh(tid);
-#pragma unroll
-    for (int c = 0; c < 5; c++) {
-      if (!pair_live(t, c)) continue;
-      const Slot sl = slot_of(t, c);
-      X_[sl.p] = osp[(2 * c) * T];
-      if (sl.pp != sl.p) X_[sl.pp] = osp[(2 * c + 1) * T];
+      for (int c = 0; c < 5; c++) {
+        if (!pair_live(t, c)) continue;
+        const Slot sl = slot_of(t, c);
+        X_[sl.p] = osp[(2 * c) * T];
+        if (sl.pp != sl.p) X_[sl.pp] = osp[(2 * c + 1) * T];
+      }
     }
-  }
-  fft8k_dit<true>(s_x, tw, tid);
+    STAMP(5 + h);
+    fft8k_dit<true>(s_x, tw, tid);
+    STAMP(6 + h);
 #pragma unroll
-  for (int q = 0; q < 8; q++) { const double2 z = X_[tid + T * q]; tho[q] = atan2(z.y, z.x); }
-  __syncthreads();
+    for (int q = 0; q < 8; q++) {
+      const double2 z = X_[tid + T * q];
+      const double a = atan2(z.y, z.x);
+      if (h) tho[q] = a;
+      else the[q] = a;
+    }
+    __syncthreads();
+  }
   double* ph = reinterpret_cast<double*>(s_x);    // plain (unswizzled) phase scratch
 #pragma unroll
   for (int q = 0; q < 8; q++) ph[tid + T * q] = tho[q];
   __syncthreads();
 
+  STAMP(8);
   // ---- 5. FM demod (Hz) -> demod spectrum D (parked in ospill) ----------------------------------
   {
     const double hzk = C.freq_hz / TAU;
@@ -329,59 +378,70 @@ extern "C" __global__ __launch_bounds__(1024) void ldg_k_demod(
 #pragma unroll
     for (int q = 0; q < 8; q++) X_[tid + T * q] = make_double2(d0[q], d1[q]);
   }
+  STAMP(9);
   fft8k_dif<false>(s_x, tw, tid);
+  STAMP(10);
   Pairs D;
   split_pairs(X_, twk, tid, D);
   __syncthreads();
+  STAMP(11);
 
+  // ---- 6. output channels: video, burst, [pilot], 0.5 MHz (its output is the
+  // sync detector's input), then sync from the detector's own spectrum.  One
+  // loop body: one copy of the inverse FFT in the code.
   const double inv = 1.0 / (double)M;
-  auto emit = [&](int ch, const double2* G) {
+  const int nout = C.n_chan > 4 ? 5 : 4;
+#pragma clang loop unroll(disable)
+  for (int e = 0; e < nout; e++) {
+    const int kind = (C.n_chan > 4 || e < 2) ? e : e + 1;   // 0 video, 1 burst, 2 pilot, 3 0.5 MHz, 4 sync
+    const double2* G = kind == 0 ? g_video : kind == 1 ? g_burst : kind == 2 ? g_pilot : kind == 3 ? g_05 : g_psync;
     merge_pairs(X_, twk, G, tid, D);
+    STAMP(12 + 3 * e);
     fft8k_dit<true>(s_x, tw, tid);
-    double* o = vout + (int64_t)ch * vchan_stride;
+    STAMP(13 + 3 * e);
     const int t = fresh(tid);
+    if (kind != 3) {
+      const int ch = kind == 0 ? CH_DEMOD : kind == 1 ? CH_BURST : kind == 2 ? CH_PILOT : CH_SYNC;
+      double* o = vout + (int64_t)ch * vchan_stride;
 #pragma unroll
-    for (int q = 0; q < 8; q++) {
-      const int m = t + T * q;
-      const int p = 2 * m;
-      const double2 z = X_[m];
-      if (p >= BLOCKCUT && p < BLOCKCUT + copylen) o[p] = z.x * inv;
-      if (p + 1 >= BLOCKCUT && p + 1 < BLOCKCUT + copylen) o[p + 1] = z.y * inv;
+      for (int q = 0; q < 8; q++) {
+        const int m = t + T * q;
+        const int p = 2 * m;
+        const double2 z = X_[m];
+        const bool in0 = p >= BLOCKCUT && p < BLOCKCUT + copylen;
+        const bool in1 = p + 1 >= BLOCKCUT && p + 1 < BLOCKCUT + copylen;
+        if (in0 && in1) *reinterpret_cast<double2*>(o + p) = make_double2(z.x * inv, z.y * inv);
+        else if (in0) o[p] = z.x * inv;
+        else if (in1) o[p + 1] = z.y * inv;
+      }
+      __syncthreads();
+    } else {
+      double v0[8], v1[8];
+#pragma unroll
+      for (int q = 0; q < 8; q++) { const double2 z = X_[t + T * q]; v0[q] = z.x * inv; v1[q] = z.y * inv; }
+      __syncthreads();
+      double* o = vout + (int64_t)CH_05 * vchan_stride;
+#pragma unroll
+      for (int q = 0; q < 8; q++) {
+        const int m = t + T * q;
+        // value at block position p lands at rolled position (p - 32) mod 16384 (even: p0 + 1 never wraps)
+        const int p0 = (2 * m - BLOCKCUT_END) & (BLOCKLEN - 1);
+        const bool in0 = p0 >= BLOCKCUT && p0 < BLOCKCUT + copylen;
+        const bool in1 = p0 + 1 >= BLOCKCUT && p0 + 1 < BLOCKCUT + copylen;
+        if (in0 && in1) *reinterpret_cast<double2*>(o + p0) = make_double2(v0[q], v1[q]);
+        else if (in0) o[p0] = v0[q];
+        else if (in1) o[p0 + 1] = v1[q];
+        // inrange(demod_05, iretohz(-55), iretohz(-25)) as 0/1 doubles
+        const int mz = (m - BLOCKCUT_END / 2) & (M - 1);
+        X_[mz] = make_double2((v0[q] >= C.sync_lo && v0[q] <= C.sync_hi) ? 1.0 : 0.0,
+                              (v1[q] >= C.sync_lo && v1[q] <= C.sync_hi) ? 1.0 : 0.0);
+      }
+      fft8k_dif<false>(s_x, tw, tid);
+      split_pairs(X_, twk, tid, D);
+      __syncthreads();
     }
-    __syncthreads();
-  };
-  emit(CH_DEMOD, g_video);
-  emit(CH_BURST, g_burst);
-  if (C.n_chan > 4) emit(CH_PILOT, g_pilot);
-
-  // ---- 6. 0.5 MHz channel (rolled by -F05_offset) and the sync detector --------
-  merge_pairs(X_, twk, g_05, tid, D);
-  fft8k_dit<true>(s_x, tw, tid);
-  {
-    double v0[8], v1[8];
-#pragma unroll
-    for (int q = 0; q < 8; q++) { const double2 z = X_[tid + T * q]; v0[q] = z.x * inv; v1[q] = z.y * inv; }
-    __syncthreads();
-    double* o = vout + (int64_t)CH_05 * vchan_stride;
-    const int t = fresh(tid);
-#pragma unroll
-    for (int q = 0; q < 8; q++) {
-      const int m = t + T * q;
-      // value at block position p lands at rolled position (p - 32) mod 16384
-      const int p0 = (2 * m - BLOCKCUT_END) & (BLOCKLEN - 1);
-      const int p1 = (2 * m + 1 - BLOCKCUT_END) & (BLOCKLEN - 1);
-      if (p0 >= BLOCKCUT && p0 < BLOCKCUT + copylen) o[p0] = v0[q];
-      if (p1 >= BLOCKCUT && p1 < BLOCKCUT + copylen) o[p1] = v1[q];
-      // inrange(demod_05, iretohz(-55), iretohz(-25)) as 0/1 doubles
-      const int mz = (m - BLOCKCUT_END / 2) & (M - 1);
-      X_[mz] = make_double2((v0[q] >= C.sync_lo && v0[q] <= C.sync_hi) ? 1.0 : 0.0,
-                            (v1[q] >= C.sync_lo && v1[q] <= C.sync_hi) ? 1.0 : 0.0);
-    }
+    STAMP(14 + 3 * e);
   }
-  fft8k_dif<false>(s_x, tw, tid);
-  split_pairs(X_, twk, tid, D);
-  __syncthreads();
-  emit(CH_SYNC, g_psync);
 }
 
 // ---------------------------------------------------------------------------

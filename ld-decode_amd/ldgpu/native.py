@@ -69,11 +69,13 @@ class Filters(C.Structure):
 _lib = None
 
 
-def load(path=LIB_PATH):
-    """Load libldgpu.so and declare its signatures (no device access)."""
+def load(path=None):
+    """Load libldgpu.so and declare its signatures (no device access).
+    LDGPU_LIB names another build of the same library (profiling variants)."""
     global _lib
     if _lib is not None:
         return _lib
+    path = path or os.environ.get('LDGPU_LIB') or LIB_PATH
     if not os.path.exists(path):
         raise RuntimeError('libldgpu.so not built (%s); run __graft_entry__.build()' % path)
     lib = C.CDLL(path)
