@@ -6,14 +6,23 @@
 // :523-553, ToRGB :555-598 (RGB::conv :124-147), PostProcess :894-938.
 //
 // Every output row depends only on its own line and the lines two above and
-// below it (the 2D stencil).  That holds with one exception: the burst-level
-// EMA `aburstlev` is a recurrence over all lines of all frames in order, so a
-// one-wave kernel runs that chain first.  DoYNR's FIR history crosses lines
-// and frames in the reference, but for output pixels (x >= 78) all 25 taps
-// fall inside the same line (h - 12 >= 66 >= 40), so the history never
-// reaches an output pixel.  One workgroup per (frame, output row) runs
-// SplitIQ -> AdjustY -> FilterIQ (two sequential 1-pole chains, as in the
-// reference) -> Y-NR -> YIQ->RGB with the row in LDS.
+// below it (the 2D stencil), with two exceptions that are sequential
+// recurrences: the burst-level EMA `aburstlev` over all lines of all frames
+// (ldg_k_comb_burst, one lane), and FilterIQ's two 1-pole chains per line
+// (418 feeds each).  DoYNR's FIR history crosses lines and frames in the
+// reference, but for output pixels (x >= 78) all 25 taps fall inside the same
+// line (h - 12 >= 66 >= 40), so the history never reaches an output pixel.
+//
+// Three row kernels, so that no workgroup holds a CU's LDS while one lane
+// runs a 418-step chain:
+//   ldg_k_comb_split  one workgroup per (frame, row): raw rows l-2, l, l+2 in
+//                     LDS -> Split1D / Split2D -> the signed chroma cv[h] of
+//                     SplitIQ, written to HBM (910 doubles per row);
+//   ldg_k_comb_iq     one LANE per FilterIQ chain (row, I or Q): reads the held
+//                     I / Q feeds from cv, runs the recurrence in the
+//                     reference's arithmetic order, writes the 418 outputs;
+//   ldg_k_comb_out    one workgroup per (frame, row): AdjustY from the raw line
+//                     and cv, the FilterIQ outputs, DoYNR, YIQ -> RGB.
 #include <hip/hip_runtime.h>
 #include "common.hpp"
 
@@ -23,6 +32,9 @@ namespace comb {
 constexpr int IN_X = 910, IN_Y = 525;
 constexpr int OUT_W = 744, OUT_H = 480, OUT_X0 = 78, FIRST_LINE = 38;
 constexpr int CHAIN_LINES = IN_Y - FIRST_LINE;            // 487 lines feed aburstlev per frame
+constexpr int CV_STRIDE = 912;                             // doubles per row of the cv buffer
+constexpr int IQ_ROW0 = 44 - FIRST_LINE;                   // first output row with FilterIQ (line 44)
+constexpr int IQ_ROWS = OUT_H - IQ_ROW0;                   // 474 rows per frame run the chains
 constexpr double IRESCALE = 358.4, IREBASE = 1024.0;
 constexpr double BLACK_IRE = 7.5, BRIGHTNESS = 236.0;
 constexpr double NR_Y = 1.0 * IRESCALE;
@@ -41,14 +53,6 @@ __constant__ NRTaps g_nr = {{
     1.141291975113614e-04}};
 
 __device__ __forceinline__ double clampd(double v, double lo, double hi) { return v < lo ? lo : (v > hi ? hi : v); }
-
-// Split1D's tc1 of row r (0 outside lines 44..524 / pixels 4..839): integer average.
-__device__ __forceinline__ double clp0(const uint16_t* __restrict__ fr, int r, int h) {
-  if (r < 44 || r >= IN_Y || h < 4 || h >= 840) return 0.0;
-  const uint16_t* line = fr + r * IN_X;
-  const int avg = ((int)line[h + 2] + (int)line[h - 2]) / 2;
-  return (double)(avg - (int)line[h]);
-}
 
 // clp1 with the three clp0 rows staged in LDS (p = l-2, c = l, n = l+2).
 __device__ __forceinline__ double clp1_lds(const double* p1, const double* c1, const double* n1, int h) {
@@ -87,35 +91,23 @@ __device__ __forceinline__ double u16_to_ire_of(double v) {
   return -40 + ((double)level - IREBASE) / IRESCALE;
 }
 
-// FilterIQ's 1-pole colorlpi chain over one of I (even h) / Q (odd h): every h
-// writes the latest output two pixels back, so the feed at h fills h-2 and
-// h-1.  Inputs are prefetched 16 at a time so only the recurrence is serial.
-template <bool Q>
-__device__ __forceinline__ void iq_chain(const double* __restrict__ src, double* __restrict__ dst) {
-  double x0 = 0, x1 = 0, y1 = 0;
-  if (Q) dst[2] = 0.0;                     // h = 4 writes the not-yet-fed Q output
-  constexpr int H0 = Q ? 5 : 4;
-  for (int hb = H0; hb < 840; hb += 32) {
-    double xs[16];
-#pragma unroll
-    for (int k = 0; k < 16; k++) { const int h = hb + 2 * k; xs[k] = (h < 840) ? src[h] : 0.0; }
-#pragma unroll
-    for (int k = 0; k < 16; k++) {
-      const int h = hb + 2 * k;
-      if (h < 840) {
-        x1 = x0;
-        x0 = xs[k];
-        double y0 = 0;
-        y0 += (LPI_B0 / 1.0) * x0;
-        y0 += (LPI_B1 / 1.0) * x1;
-        y0 -= (LPI_A1 / 1.0) * y1;
-        y1 = y0;
-        dst[h - 2] = y0;
-        if (h + 1 < 840) dst[h - 1] = y0;
-      }
-    }
-  }
+// SplitIQ's held I / Q at pixel p (0 outside [4, 840)) from the signed chroma cv.
+__device__ __forceinline__ double held_i(const double* __restrict__ cv, int p) {
+  if (p < 4 || p >= 840) return 0.0;
+  const int he = p & ~1;                 // latest even h' <= p (phase 0 / 2)
+  return ((he & 3) == 0) ? cv[he] : -cv[he];
 }
+__device__ __forceinline__ double held_q(const double* __restrict__ cv, int p) {
+  if (p < 4 || p >= 840) return 0.0;
+  const int ho = (p & 1) ? p : p - 1;    // latest odd h' <= p (phase 1 / 3), none before 5
+  if (ho < 5) return 0.0;
+  return ((ho & 3) == 1) ? -cv[ho] : cv[ho];
+}
+
+// FilterIQ's colorlpi chains: feeds h = H0 + 2k < 840 (H0 = 4 for I, 5 for Q),
+// k < 418; the feed at h writes its output to pixels h-2 and h-1 (h-1 only
+// while h+1 < 840; Q's pixel 2 is never fed and reads 0).
+constexpr int IQ_NS = 418;
 
 }  // namespace comb
 }  // namespace ldg
@@ -133,8 +125,10 @@ constexpr int BURST_CHUNK = 4096;
 extern "C" __global__ __launch_bounds__(256) void ldg_k_comb_burst(const uint16_t* __restrict__ frames, int n,
                                                                    double* __restrict__ state,
                                                                    double* __restrict__ abl) {
-  __shared__ double s_b[BURST_CHUNK];
-  __shared__ double s_a[BURST_CHUNK];
+  prio_latency();
+
+  __shared__ __align__(16) double s_b[BURST_CHUNK];
+  __shared__ __align__(16) double s_a[BURST_CHUNK];
   const int tid = threadIdx.x;
   double a = state[0];
   const int total = n * CHAIN_LINES;
@@ -156,14 +150,31 @@ extern "C" __global__ __launch_bounds__(256) void ldg_k_comb_burst(const uint16_
         }
         s_a[k] = a;
       }
-      // a > 0 from here on (burst levels > 3): only the EMA is on the serial path
-#pragma unroll 8
-      for (; k < cnt; k++) {
-        const double bk = s_b[k];
+      // a > 0 from here on (burst levels > 3): only the EMA is on the serial path;
+      // levels are read and results written 16 at a time (16-byte LDS accesses)
+      auto step = [&](double bk) {
         const double e = (a * .99) + (bk * .01);
         a = (bk > 3) ? e : a;
-        s_a[k] = a;
+        return a;
+      };
+      if (k < cnt && (k & 1)) { s_a[k] = step(s_b[k]); k++; }
+#pragma unroll 1
+      for (; k + 16 <= cnt; k += 16) {
+        double bs[16];
+#pragma unroll
+        for (int j = 0; j < 16; j += 2) {
+          const double2 v = *reinterpret_cast<const double2*>(s_b + k + j);
+          bs[j] = v.x;
+          bs[j + 1] = v.y;
+        }
+#pragma unroll
+        for (int j = 0; j < 16; j += 2) {
+          const double a0 = step(bs[j]);
+          const double a1 = step(bs[j + 1]);
+          *reinterpret_cast<double2*>(s_a + k + j) = make_double2(a0, a1);
+        }
       }
+      for (; k < cnt; k++) s_a[k] = step(s_b[k]);
     }
     __syncthreads();
     for (int k = tid; k < cnt; k += 256) abl[c0 + k] = s_a[k];
@@ -172,30 +183,41 @@ extern "C" __global__ __launch_bounds__(256) void ldg_k_comb_burst(const uint16_
   if (tid == 0) state[0] = a;
 }
 
-// One output row: grid n * 480 workgroups of 256 threads; row r = line r + 38.
-extern "C" __global__ __launch_bounds__(256) void ldg_k_comb_rows(const uint16_t* __restrict__ frames,
-                                                                  const double* __restrict__ abl,
-                                                                  uint16_t* __restrict__ rgb) {
-  __shared__ double s_c[3][IN_X];                        // Split1D clp0 of rows l-2, l, l+2
-  __shared__ double s_y[IN_X], s_i[IN_X], s_q[IN_X];    // cbuf after SplitIQ / AdjustY
-  __shared__ double s_cv[IN_X];                          // signed chroma per pixel (before the hold)
-  double* const s_fi = s_c[0];                           // FilterIQ output (clp0 rows are dead by then)
-  double* const s_fq = s_c[1];
+// ---- ldg_k_comb_split: SplitIQ's signed chroma of one row.
+// grid: n * 480 workgroups of 256 threads; row r = line r + 38; cv: [n][480][CV_STRIDE].
+extern "C" __global__ __launch_bounds__(256) void ldg_k_comb_split(const uint16_t* __restrict__ frames,
+                                                                   double* __restrict__ cvbuf) {
+  __shared__ uint16_t s_raw[3][IN_X + 2];                // raw lines l-2, l, l+2
+  __shared__ double s_c[3][IN_X];                        // Split1D clp0 of those lines
   const int tid = threadIdx.x;
   const int f = blockIdx.x / OUT_H;
   const int row = blockIdx.x % OUT_H;
   const int l = row + FIRST_LINE;
   const uint16_t* fr = frames + (size_t)f * IN_X * IN_Y;
-  const uint16_t* line = fr + (size_t)l * IN_X;
-  const bool invertphase = (line[0] == 16384);
-
-  for (int h = tid; h < IN_X; h += 256) {
-#pragma unroll
-    for (int k = 0; k < 3; k++) s_c[k][h] = clp0(fr, l - 2 + 2 * k, h);
+  // lines are 1820 B apart: 4-byte loads are aligned
+  for (int t = tid; t < 3 * (IN_X / 2); t += 256) {
+    const int k = t / (IN_X / 2), w = t % (IN_X / 2);
+    const uint32_t v = reinterpret_cast<const uint32_t*>(fr + (size_t)(l - 2 + 2 * k) * IN_X)[w];
+    s_raw[k][2 * w] = (uint16_t)(v & 0xffff);
+    s_raw[k][2 * w + 1] = (uint16_t)(v >> 16);
   }
   __syncthreads();
-  // ---- SplitIQ: chroma samples (Split2D / Split1D weights), then the held I / Q
   for (int h = tid; h < IN_X; h += 256) {
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+      const int r = l - 2 + 2 * k;
+      double c = 0.0;
+      if (r >= 44 && r < IN_Y && h >= 4 && h < 840) {
+        const int avg = ((int)s_raw[k][h + 2] + (int)s_raw[k][h - 2]) / 2;   // integer average (Split1D)
+        c = (double)(avg - (int)s_raw[k][h]);
+      }
+      s_c[k][h] = c;
+    }
+  }
+  __syncthreads();
+  const bool invertphase = (s_raw[1][0] == 16384);
+  double* cvrow = cvbuf + ((size_t)f * OUT_H + row) * CV_STRIDE;
+  for (int h = tid; h < CV_STRIDE; h += 256) {
     double cv = 0.0;
     if (h >= 4 && h < 840) {
       double cavg = 0;
@@ -211,60 +233,103 @@ extern "C" __global__ __launch_bounds__(256) void ldg_k_comb_rows(const uint16_t
       if (!invertphase) cavg = -cavg;
       cv = cavg;
     }
-    s_cv[h] = cv;
+    cvrow[h] = cv;
   }
-  __syncthreads();
-  for (int h = tid; h < IN_X; h += 256) {
-    double y = 0, si = 0, sq = 0;
-    if (h >= 4 && h < 840) {
-      y = line[h];
-      const int he = h & ~1;                 // latest even h' <= h (phase 0 / 2)
-      si = ((he & 3) == 0) ? s_cv[he] : -s_cv[he];
-      const int ho = (h & 1) ? h : h - 1;    // latest odd h' <= h (phase 1 / 3), none before 5
-      if (ho >= 5) sq = ((ho & 3) == 1) ? -s_cv[ho] : s_cv[ho];
-    }
-    s_y[h] = y; s_i[h] = si; s_q[h] = sq;
-  }
-  __syncthreads();
-  // ---- AdjustY: p[h] = p[h + 2] with y += +-I / +-Q (h in [2, 842))
-  double ay[4], ai[4], aq[4];
+}
+
+// ---- ldg_k_comb_iq: FilterIQ's two chains of every row with line >= 44, one
+// lane each.  Feed h: x_h = AdjustY's I (Q) at h = the held value at h + 2;
+// y = ((0 + b0 x_h) + b1 x_{h-2}) - a1 y_prev in the reference's order
+// (Filter::feed, ld-decoder.h:180-186).  grid: ceil(n * 474 * 2 / 256) x 256.
+// iq: [n][474][2][IQ_NS] outputs.
+extern "C" __global__ __launch_bounds__(256) void ldg_k_comb_iq(const double* __restrict__ cvbuf, int n,
+                                                                double* __restrict__ iq) {
+  prio_latency();
+
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= n * IQ_ROWS * 2) return;
+  const int q = c & 1, rr = (c >> 1) % IQ_ROWS, f = (c >> 1) / IQ_ROWS;
+  const double* cv = cvbuf + ((size_t)f * OUT_H + IQ_ROW0 + rr) * CV_STRIDE;
+  double* out = iq + (((size_t)f * IQ_ROWS + rr) * 2 + q) * IQ_NS;
+  // feed k reads the held value at p = H0 + 2k + 2: I (p = 6 + 2k, even) is
+  // -cv[p] for even k and +cv[p] for odd k; Q (p = 7 + 2k, odd) is +cv[p] for
+  // even k and -cv[p] for odd k; both are 0 at p >= 840 (k = 417).  Lanes c
+  // and c + 1 (I and Q of one row) read the same pairs (cv[6 + 2k], cv[7 + 2k]).
+  const double2* cv2 = reinterpret_cast<const double2*>(cv) + 3;
+  double x1 = 0.0, y1 = 0.0;
+#pragma unroll 1
+  for (int kb = 0; kb < IQ_NS; kb += 16) {
+    double xs[16];
 #pragma unroll
-  for (int e = 0; e < 4; e++) {
-    const int h = tid + 256 * e;
-    if (h >= IN_X) continue;
-    if (h >= 2 && h < 842) {
-      const double yy = s_y[h + 2], ii = s_i[h + 2], qq = s_q[h + 2];
-      double comp = 0;
-      switch (h & 3) {
-        case 0: comp = ii; break;
-        case 1: comp = -qq; break;
-        case 2: comp = -ii; break;
-        default: comp = qq; break;
+    for (int j = 0; j < 16; j++) {
+      const int k = kb + j;
+      const double2 v = cv2[k < IQ_NS - 1 ? k : 0];
+      const double x = q ? v.y : v.x;
+      xs[j] = (k >= IQ_NS - 1) ? 0.0 : (((k & 1) != q) ? x : -x);
+    }
+#pragma unroll
+    for (int j = 0; j < 16; j += 2) {
+      if (kb + j < IQ_NS) {
+        double ya = 0;
+        ya += (LPI_B0 / 1.0) * xs[j];
+        ya += (LPI_B1 / 1.0) * x1;
+        ya -= (LPI_A1 / 1.0) * y1;
+        double yb = 0;
+        yb += (LPI_B0 / 1.0) * xs[j + 1];
+        yb += (LPI_B1 / 1.0) * xs[j];
+        yb -= (LPI_A1 / 1.0) * ya;
+        x1 = xs[j + 1];
+        y1 = yb;
+        *reinterpret_cast<double2*>(out + kb + j) = make_double2(ya, yb);
       }
-      if (invertphase) comp = -comp;
-      ay[e] = yy + comp; ai[e] = ii; aq[e] = qq;
-    } else {
-      ay[e] = s_y[h]; ai[e] = s_i[h]; aq[e] = s_q[h];
     }
   }
-  __syncthreads();
-#pragma unroll
-  for (int e = 0; e < 4; e++) {
-    const int h = tid + 256 * e;
-    if (h < IN_X) { s_y[h] = ay[e]; s_i[h] = ai[e]; s_q[h] = aq[e]; s_fi[h] = ai[e]; s_fq[h] = aq[e]; }
+}
+
+// ---- ldg_k_comb_out: AdjustY, the FilterIQ outputs, DoYNR and ToRGB of one row.
+// grid: n * 480 workgroups of 256 threads.
+extern "C" __global__ __launch_bounds__(256) void ldg_k_comb_out(const uint16_t* __restrict__ frames,
+                                                                 const double* __restrict__ cvbuf,
+                                                                 const double* __restrict__ iq,
+                                                                 const double* __restrict__ abl,
+                                                                 uint16_t* __restrict__ rgb) {
+  __shared__ uint16_t s_line[IN_X + 2];
+  __shared__ double s_y[IN_X];                           // AdjustY's Y
+  const int tid = threadIdx.x;
+  const int f = blockIdx.x / OUT_H;
+  const int row = blockIdx.x % OUT_H;
+  const int l = row + FIRST_LINE;
+  const uint16_t* line = frames + (size_t)f * IN_X * IN_Y + (size_t)l * IN_X;
+  for (int w = tid; w < IN_X / 2; w += 256) {
+    const uint32_t v = reinterpret_cast<const uint32_t*>(line)[w];
+    s_line[2 * w] = (uint16_t)(v & 0xffff);
+    s_line[2 * w + 1] = (uint16_t)(v >> 16);
   }
   __syncthreads();
-  // ---- FilterIQ (lines >= 44): a fresh colorlpi IIR for I (fed at even h) and
-  //      for Q (odd h); every h writes the latest output two pixels back, so
-  //      each feed at h fills positions h-2 and h-1.  Thread 0: I, thread 64: Q.
-  if (l >= 44) {
-    if (tid == 0) iq_chain<false>(s_i, s_fi);
-    if (tid == 64) iq_chain<true>(s_q, s_fq);
+  const bool invertphase = (s_line[0] == 16384);
+  const double* cv = cvbuf + ((size_t)f * OUT_H + row) * CV_STRIDE;
+  // ---- AdjustY: p[h] = p[h + 2] with y += +-I / +-Q (h in [2, 842)); only
+  //      h in [66, 834) reaches an output pixel (DoYNR taps h-12..h+12)
+  for (int h = 66 + tid; h < 834; h += 256) {
+    const int p = h + 2;
+    const double yy = (p >= 4 && p < 840) ? (double)s_line[p] : 0.0;
+    const double ii = held_i(cv, p), qq = held_q(cv, p);
+    double comp = 0;
+    switch (h & 3) {
+      case 0: comp = ii; break;
+      case 1: comp = -qq; break;
+      case 2: comp = -ii; break;
+      default: comp = qq; break;
+    }
+    if (invertphase) comp = -comp;
+    s_y[h] = yy + comp;
   }
   __syncthreads();
   // ---- DoYNR (taps inside this line for x >= 78) + ToRGB
   const double aburst = abl[(size_t)f * CHAIN_LINES + (l - FIRST_LINE)];
   const double m = BRIGHTNESS * 256 / 100;
+  const double* iqI = (l >= 44) ? iq + (((size_t)f * IQ_ROWS + (row - IQ_ROW0)) * 2 + 0) * IQ_NS : nullptr;
+  const double* iqQ = iqI ? iqI + IQ_NS : nullptr;
   uint16_t* out = rgb + ((size_t)f * OUT_H + row) * OUT_W * 3;
   for (int x = tid; x < OUT_W; x += 256) {
     const int h = x + OUT_X0;
@@ -274,7 +339,16 @@ extern "C" __global__ __launch_bounds__(256) void ldg_k_comb_rows(const uint16_t
     double a = y0;
     if (fabs(a) > NR_Y) a = (a > 0) ? NR_Y : -NR_Y;
     const double yv = s_y[h] - a;
-    double iv = s_fi[h], qv = s_fq[h];
+    // FilterIQ output at h (lines >= 44): I from feed (h - 2) / 2, Q from feed (h - 3) / 2;
+    // otherwise AdjustY's I / Q (the held values at h + 2)
+    double iv, qv;
+    if (iqI) {
+      iv = iqI[(h - 2) >> 1];
+      qv = iqQ[(h - 3) >> 1];
+    } else {
+      iv = held_i(cv, h + 2);
+      qv = held_q(cv, h + 2);
+    }
     iv *= (10 / aburst);
     qv *= (10 / aburst);
     double y = u16_to_ire_of(yv);

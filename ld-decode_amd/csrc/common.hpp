@@ -76,4 +76,28 @@ struct SysConst {
   int32_t pad_;
 };
 
+// Latency-bound kernels (a wave per read / per line, one lane per recurrence)
+// share CUs with the FP64-throughput demod; raise their wave priority so the
+// SIMD arbiter issues their serial chains first (demod waves fill the gaps).
+__device__ __forceinline__ void prio_latency() { __builtin_amdgcn_s_setprio(3); }
+
 }  // namespace ldg
+
+// Per-kernel phase stamps (profiling builds only, -DLDG_STAMPS; tools/kstamps.py):
+// thread 0 of the first KST_BLOCKS workgroups of kernel K records the shader
+// clock at phase boundary i (after a workgroup barrier).
+// K: 0 comb_rows, 1 final_lines, 2 burst_field, 3 sync, 4 burst_lines, 5 philips.
+#ifdef LDG_STAMPS
+constexpr int KST_KERNELS = 6, KST_BLOCKS = 4096, KST_PHASES = 16;
+__device__ unsigned long long g_kst[KST_KERNELS][KST_BLOCKS][KST_PHASES];
+#define KSTAMP(K, i)                                                               \
+  do {                                                                             \
+    __syncthreads();                                                               \
+    if (threadIdx.x == 0 && blockIdx.x < KST_BLOCKS)                               \
+      g_kst[K][blockIdx.x][i] = __builtin_readcyclecounter();                      \
+  } while (0)
+#else
+#define KSTAMP(K, i) \
+  do {               \
+  } while (0)
+#endif

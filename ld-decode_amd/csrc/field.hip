@@ -111,6 +111,8 @@ extern "C" __global__ __launch_bounds__(64) void ldg_k_sync_walk(
     int64_t vread_stride, int64_t vchan_stride, SysConst C, const int32_t* __restrict__ status,
     int32_t* __restrict__ node_pos, int32_t* __restrict__ node_pk, double* __restrict__ node_lv,
     int32_t* __restrict__ node_n) {
+  prio_latency();
+
   const int lane = threadIdx.x;
   const int slot = smap[blockIdx.x / SEG_K];
   const int k = blockIdx.x % SEG_K;
@@ -149,6 +151,8 @@ extern "C" __global__ __launch_bounds__(64) void ldg_k_sync(
     int64_t vchan_stride, SysConst C, FieldRec* __restrict__ recs, int32_t* __restrict__ peaks,
     const int32_t* __restrict__ status, const int32_t* __restrict__ node_pos, const int32_t* __restrict__ node_pk,
     const double* __restrict__ node_lv, const int32_t* __restrict__ node_n) {
+  prio_latency();
+
   __shared__ int32_t s_npos[SEG_K * SEG_NMAX];
   __shared__ int32_t s_npk[SEG_K * SEG_NMAX];
   __shared__ int32_t s_cnt[SEG_K];
@@ -394,6 +398,8 @@ extern "C" __global__ __launch_bounds__(64) void ldg_k_linelocs(
     const int32_t* __restrict__ smap, const double* __restrict__ video, int64_t vread_stride, int64_t vchan_stride, SysConst C,
     FieldRec* __restrict__ recs, const int32_t* __restrict__ peaks, double* __restrict__ lines,
     int8_t* __restrict__ bad) {
+  prio_latency();
+
   __shared__ double s_key[LINENUM_SPAN];
   __shared__ uint8_t s_has[LINENUM_SPAN];
   __shared__ uint8_t s_orig[LINENUM_SPAN];
@@ -581,6 +587,8 @@ extern "C" __global__ __launch_bounds__(64) void ldg_k_linelocs(
 extern "C" __global__ __launch_bounds__(64) void ldg_k_hsync_lines(
     const int32_t* __restrict__ smap, const double* __restrict__ video, int64_t vread_stride, int64_t vchan_stride, SysConst C,
     FieldRec* __restrict__ recs, double* __restrict__ lines, int8_t* __restrict__ bad) {
+  prio_latency();
+
   __shared__ double s_tmp[20];
   const int lane = threadIdx.x;
   const int slot = smap[blockIdx.x / MAX_LINES];
@@ -657,6 +665,8 @@ extern "C" __global__ __launch_bounds__(256) void ldg_k_hsync_field(const int32_
                                                                    FieldRec* __restrict__ recs,
                                                                    double* __restrict__ lines,
                                                                    int8_t* __restrict__ bad) {
+  prio_latency();
+
   __shared__ double s_v[MAX_LINES];
   __shared__ int8_t s_bad[MAX_LINES];
   __shared__ int s_err;
@@ -711,6 +721,8 @@ extern "C" __global__ __launch_bounds__(256) void ldg_k_hsync_field(const int32_
 extern "C" __global__ __launch_bounds__(64) void ldg_k_philips(
     const int32_t* __restrict__ smap, const double* __restrict__ video, int64_t vread_stride, int64_t vchan_stride, SysConst C,
     FieldRec* __restrict__ recs, const double* __restrict__ lines) {
+  prio_latency();
+
   __shared__ int32_t s_code[3][6];
   __shared__ int32_t s_ok[3];
   const int lane = threadIdx.x;

@@ -98,9 +98,10 @@ __device__ __forceinline__ double block_affine_carry(double A, double B, bool su
   return c;
 }
 
-template <int NT, class SL, class Sink>
+template <int NT, int STK = -1, class SL, class Sink>
 __device__ int spline_block(const double* __restrict__ buf, int64_t len, double begin, double end, int W, int o_lo,
                             int o_hi, int tid, SL& S, Sink&& sink) {
+  if constexpr (STK >= 0) KSTAMP(STK, 0);
   if (tid < 17) S.ct[tid] = g_ctab.v[tid];
   const int64_t ib = py_int(begin), ie = py_int(end);
   const int64_t n64 = ie - ib;
@@ -129,6 +130,7 @@ __device__ int spline_block(const double* __restrict__ buf, int64_t len, double 
     S.mn1 = (6.0 * ((y[n] - y[n - 1]) - (y[n - 1] - y[n - 2]))) / 6.0;
   }
   __syncthreads();
+  if constexpr (STK >= 0) KSTAMP(STK, 1);
   const double M1 = S.m1, Mn1 = S.mn1;
   const double BL = (lo == 2) ? M1 : 0.0, BR = (hi == n - 2) ? Mn1 : 0.0;
   const int T = hi - lo + 1;                                  // rows j = lo + t
@@ -152,6 +154,7 @@ __device__ int spline_block(const double* __restrict__ buf, int64_t len, double 
     B = (rhs(t) - B) * c;
   }
   double dprev = block_affine_carry<NT>(A, B, false, tid, S);
+  if constexpr (STK >= 0) KSTAMP(STK, 2);
   for (int t = t0; t < t1; t++) {
     const double d = (rhs(t) - dprev) * ct(t);
     ms[lo + t] = d;
@@ -164,7 +167,9 @@ __device__ int spline_block(const double* __restrict__ buf, int64_t len, double 
     A = -c * A;
     B = ms[lo + t] - c * B;
   }
+  if constexpr (STK >= 0) KSTAMP(STK, 3);
   double Mnext = block_affine_carry<NT>(A, B, true, tid, S);
+  if constexpr (STK >= 0) KSTAMP(STK, 4);
   for (int t = t1 - 1; t >= t0; t--) {
     const double M = ms[lo + t] - ct(t) * Mnext;
     ms[lo + t] = M;
@@ -176,6 +181,7 @@ __device__ int spline_block(const double* __restrict__ buf, int64_t len, double 
     if (hi == n - 2) { ms[n - 1] = Mn1; if (top == n) ms[n] = 2.0 * Mn1 - ms[n - 2]; }
   }
   __syncthreads();
+  if constexpr (STK >= 0) KSTAMP(STK, 5);
   for (int o = o_lo + tid; o < o_hi; o += NT) {
     const double x = xo(o);
     const int k = ival(x);
@@ -184,6 +190,7 @@ __device__ int spline_block(const double* __restrict__ buf, int64_t len, double 
     const double v = Mk * a * a * a / 6.0 + Mk1 * b * b * b / 6.0 + (yk - Mk / 6.0) * a + (yk1 - Mk1 / 6.0) * b;
     sink(o, v);
   }
+  if constexpr (STK >= 0) KSTAMP(STK, 6);
   return 0;
 }
 
@@ -213,6 +220,8 @@ __device__ inline int calczc_s(const double* d, int len, int s, double target, i
 extern "C" __global__ __launch_bounds__(64) void ldg_k_burst_lines(
     const int32_t* __restrict__ smap, const double* __restrict__ video, int64_t vread_stride, int64_t vchan_stride, SysConst C,
     FieldRec* __restrict__ recs, double* __restrict__ lines, float* __restrict__ blevel, int pass) {
+  prio_latency();
+
   // window rows for 40 outputs: <= 40 * SPL_MAXN / W + 2 * KTR + 4 < 384
   __shared__ SplineLDS<64, 384> S;
   __shared__ double s_ba[40], s_t[40], s_g[2][40];
@@ -307,6 +316,8 @@ extern "C" __global__ __launch_bounds__(64) void ldg_k_burst_field(const int32_t
                                                                    double* __restrict__ lines,
                                                                    float* __restrict__ blevel, SysConst C,
                                                                    int pass) {
+  prio_latency();
+
   __shared__ double s_c0[512], s_c1[512];
   __shared__ int s_nc;
   const int lane = threadIdx.x;
@@ -373,6 +384,8 @@ extern "C" __global__ __launch_bounds__(FINAL_NT) void ldg_k_final_lines(
     const int32_t* __restrict__ smap, const double* __restrict__ video, int64_t vread_stride, int64_t vchan_stride,
     SysConst C, FieldRec* __restrict__ recs, const double* __restrict__ lines, const float* __restrict__ blevel,
     uint16_t* __restrict__ pic, int64_t pic_stride) {
+  prio_latency();
+
   __shared__ SplineLDS<FINAL_NT> S;
   const int tid = threadIdx.x;
   const int slot = smap[blockIdx.x / MAX_LINES];
@@ -393,7 +406,7 @@ extern "C" __global__ __launch_bounds__(FINAL_NT) void ldg_k_final_lines(
   const double scale_ = pal ? (double)(0xd300 - 0x0100) / (100 - C.vsync_ire)
                             : (double)(0xc800 - 0x0400) / (100 - C.vsync_ire);
   const double base = pal ? 256.0 : 1024.0;
-  const int rc = spline_block<FINAL_NT>(dm, R->n_out, b0, b1, W, 0, W, tid, S, [&](int o, double v) {
+  const int rc = spline_block<FINAL_NT, 1>(dm, R->n_out, b0, b1, W, 0, W, tid, S, [&](int o, double v) {
     double red = ((v * wow) - C.ire0) / C.hz_ire;
     red -= C.vsync_ire;
     double x = (red * scale_) + base;
@@ -513,6 +526,8 @@ extern "C" __global__ __launch_bounds__(64) void ldg_k_pilot_lines(const int32_t
                                                                    SysConst C, FieldRec* __restrict__ recs,
                                                                    double* __restrict__ lines,
                                                                    double* __restrict__ scratch) {
+  prio_latency();
+
   const int lane = threadIdx.x;
   const int slot = smap[blockIdx.x / LINE_GROUPS];
   const int grp = blockIdx.x % LINE_GROUPS;
@@ -574,6 +589,8 @@ extern "C" __global__ __launch_bounds__(256) void ldg_k_pilot_field(const int32_
                                                                     FieldRec* __restrict__ recs,
                                                                     double* __restrict__ lines, SysConst C,
                                                                     double* __restrict__ scratch) {
+  prio_latency();
+
   __shared__ double s_all[8192];
   __shared__ int s_n;
   const int tid = threadIdx.x;

@@ -4,3 +4,13 @@ Host side mirrors the reference interface (RFDecode / Field / Framer /
 findframe, lddecode_core.py) over the C ABI of libldgpu.so (include/ldgpu.h);
 all per-sample and per-line work runs as HIP kernels on gfx950.
 """
+
+import os as _os
+
+# A context drives 6 HIP streams (demod, 2 field-chain sub-streams, audio phase 2,
+# frame/comb output, synchronous audio output).  HIP maps streams onto
+# GPU_MAX_HW_QUEUES hardware queues (default 4); fewer queues than streams
+# serialises unrelated streams behind each other, so ask for 12 (room for 4 field-chain sub-streams) -- before the
+# HIP runtime initialises (the first HIP call in the process).
+if int(_os.environ.get('GPU_MAX_HW_QUEUES', '0') or 0) < 12:
+    _os.environ['GPU_MAX_HW_QUEUES'] = '12'

@@ -17,6 +17,7 @@ Audio offsets (:1289, :484) are a scalar recurrence computed here with the
 reference's own numpy arithmetic; the per-sample audio resampling runs on the
 GPU for all fields of a batch at once.
 """
+import os
 import time
 
 import numpy as np
@@ -130,7 +131,8 @@ class GPUDecoder:
         self.rf = RFTables(system)
         self.sysp = self.rf.system
         self.batch = batch
-        self.capacity = capacity or max(2 * batch, batch + 16)
+        # two launches in flight + the batch the host replays + the cached path
+        self.capacity = capacity or max(4 * batch, batch + 16)
         self.ctx = native.Context(system, device, max_reads=self.capacity, max_frames=self.capacity)
         self.ctx.set_filters(self.rf.params(), self.rf.tables)
         self.log = log or (lambda *a: None)
@@ -145,7 +147,9 @@ class GPUDecoder:
         self.field_nom = int(round(self.rf.freq_hz / self.sysp.fps / 2))
         self.trace = None          # diagnostics: planner steps (tools/miss_probe.py)
         self.comb, self.comb_sink = False, None
-        self.pending = None                # (keys, slots) of the outstanding decode launch
+        self.pending = []                  # (keys, slots) of the outstanding decode launches, oldest first
+        self.inflight = set()              # keys of those launches
+        self.depth = int(os.environ.get('LDG_DEPTH', '2'))   # launches kept in flight in steady state
         self.transitions = []              # audio-offset chain: linecount of each transition's field
         self.archive, self.arch_next, self.shard_frames = False, 0, []
 
@@ -231,7 +235,7 @@ class GPUDecoder:
                 steps += 1
                 key = (int(sample), cur_mtf)
                 hit = self.cache.get(key)
-                if hit is None and key not in seen:
+                if hit is None and key not in seen and key not in self.inflight:
                     seen.add(key)
                     new.append(key)
                     if len(new) >= want:
@@ -301,15 +305,19 @@ class GPUDecoder:
         return new, chain
 
     def _launch(self, keys, protect):
-        """Decode `keys` now (launch and wait)."""
+        """Decode `keys` now (launch and wait for everything outstanding)."""
         self._launch_async(keys, protect)
-        self._launch_wait()
+        while self.pending:
+            self._launch_wait()
 
     def _launch_async(self, keys, protect):
         """Start decoding `keys` into free slots, evicting least-recently-used cache
         entries not in `protect` (the reads the replay is about to consume) as
-        needed; _launch_wait() adds the records to the cache."""
+        needed; _launch_wait() adds the records of the oldest launch to the cache.
+        Slots of launches still in flight are never reused."""
         used = {v[0] for v in self.cache.values()}
+        for _, sl in self.pending:
+            used.update(sl)
         free = [s for s in range(self.capacity) if s not in used]
         if len(free) < len(keys):
             for k in [k for k in self.cache if k not in protect][:len(keys) - len(free)]:
@@ -323,16 +331,19 @@ class GPUDecoder:
         self.stats['gpu_s'] += time.perf_counter() - t0
         self.stats['batches'] += 1
         self.stats['reads'] += len(keys)
-        self.pending = (keys, slots)
+        self.pending.append((keys, slots))
+        self.inflight.update(keys)
 
     def _launch_wait(self):
-        if self.pending is None:
+        if not self.pending:
             return
-        keys, slots = self.pending
+        dh = self.stats.setdefault('inflight_at_wait', {})
+        dh[len(self.pending)] = dh.get(len(self.pending), 0) + 1
+        keys, slots = self.pending.pop(0)
         t0 = time.perf_counter()
         infos = self.ctx.decode_reads_wait()
         self.stats['wait_s'] = self.stats.get('wait_s', 0.0) + time.perf_counter() - t0
-        self.pending = None
+        self.inflight.difference_update(keys)
         import bisect
         for k, sl, inf in zip(keys, slots, infos):
             self.cache[k] = (sl, inf)
@@ -555,18 +566,23 @@ class GPUDecoder:
         while done < num_frames and self._tell() + bpf * 1.05 <= size and more(nextsample):
             # nothing known about this capture yet: learn the first fields' parity,
             # VBI and sync positions from a small launch before speculating wide
-            # (until P + 2 field starts are known the period extrapolation has nothing to use)
-            want = self.batch if len(hist) >= self.period + 2 else min(self.batch, 8 if self._hint_keys else 4)
-            tp = time.perf_counter()
-            plan, chain = self._plan(nextsample, self.mtf_level, self.last_framenr, self.last_isclv, done == 0,
-                                     want, hist)
-            self.stats['plan_s'] = self.stats.get('plan_s', 0.0) + time.perf_counter() - tp
-            if plan:
-                # decode the reads beyond the cached path while the host replays
-                # and outputs that path (the replay stops at the first pending read)
+            # (until P + 2 field starts are known the period extrapolation has nothing to use).
+            # In steady state keep `depth` launches in flight: the newer one is planned
+            # through the older one's predicted outcomes, so its demod runs on the GPU
+            # while the older one's field kernels finish and the host replays.
+            steady = len(hist) >= self.period + 2
+            depth = self.depth if steady else 1
+            launched = 0
+            while len(self.pending) < depth:
+                want = self.batch if steady else min(self.batch, 8 if self._hint_keys else 4)
+                tp = time.perf_counter()
+                plan, chain = self._plan(nextsample, self.mtf_level, self.last_framenr, self.last_isclv, done == 0,
+                                         want, hist)
+                self.stats['plan_s'] = self.stats.get('plan_s', 0.0) + time.perf_counter() - tp
+                if not plan:
+                    break
                 self._launch_async(plan, set(chain))
-                if not chain:
-                    self._launch_wait()
+                launched += 1
             frames = []
             eof = False
             t0 = time.perf_counter()
@@ -600,12 +616,13 @@ class GPUDecoder:
             tf = time.perf_counter()
             self._flush(frames, W, H, sink)
             self.stats['flush_s'] = self.stats.get('flush_s', 0.0) + time.perf_counter() - tf
-            self._launch_wait()
             done += len(frames)
             self.stats['reads_used'] += sum(len(f.fields) for f in frames)
-            if eof or (not frames and not plan):
+            if eof or (not frames and not launched and not self.pending):
                 break
-        self._launch_wait()
+            self._launch_wait()                 # the oldest launch: the replay continues into it
+        while self.pending:
+            self._launch_wait()
         self.ctx.sync()
         return done
 

@@ -139,6 +139,7 @@ class Context:
         self.max_reads = max_reads
         self.max_frames = max_frames or max_reads
         self._keep = []
+        self._pending = []          # read counts of the outstanding ldg_decode_reads_async calls
 
     def _check(self, rc, what):
         if rc != LDG_OK:
@@ -200,18 +201,19 @@ class Context:
         return list(info)
 
     def decode_reads_async(self, starts, mtfs, slots):
-        """Launch a decode (ldg_decode_reads_async); decode_reads_wait() returns its records."""
-        self._pending = (np.ascontiguousarray(starts, dtype=np.int64), np.ascontiguousarray(mtfs, dtype=np.float64),
-                         np.ascontiguousarray(slots, dtype=np.int32))
-        s, m, sl = self._pending
+        """Launch a decode (ldg_decode_reads_async, up to 2 outstanding); decode_reads_wait()
+        returns the records of the oldest outstanding one."""
+        s, m, sl = (np.ascontiguousarray(starts, dtype=np.int64), np.ascontiguousarray(mtfs, dtype=np.float64),
+                    np.ascontiguousarray(slots, dtype=np.int32))
         self._check(self.lib.ldg_decode_reads_async(self.h, s.size, s.ctypes.data, m.ctypes.data, sl.ctypes.data),
                     'ldg_decode_reads_async')
+        self._pending.append(s.size)
 
     def decode_reads_wait(self):
-        n = self._pending[0].size
+        n = self._pending[0]
         info = (FieldInfo * n)()
         self._check(self.lib.ldg_decode_reads_wait(self.h, info), 'ldg_decode_reads_wait')
-        self._pending = None
+        self._pending.pop(0)
         return list(info)
 
     def field_audio(self, slots, offsets):
