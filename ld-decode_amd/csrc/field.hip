@@ -611,7 +611,7 @@ extern "C" __global__ __launch_bounds__(64) void ldg_k_hsync_lines(
   if (i < 9) v -= 200;
   const double ll1 = v;
   double zc;
-  const int rc = wave_calczc(d05, len, v, hz(-20), 400, lane, &zc);
+  const int rc = wave_calczc_pf<7>(d05, len, v, hz(-20), 400, lane, &zc);
   if (rc < 0) { finish(v, 2); return; }
   if (rc == 0 && !lb) {
     v = zc;
@@ -624,8 +624,10 @@ extern "C" __global__ __launch_bounds__(64) void ldg_k_hsync_lines(
       bool isbad = false, raised = false;
       auto grp = [&](int64_t a, int64_t b, double lo, double hi) -> bool {
         if (a >= b) { raised = true; return true; }
-        if (wave_minmax_np(d05, a, b, false, lane) < lo) return true;
-        return wave_minmax_np(d05, a, b, true, lane) > hi;
+        double mn, mx;
+        wave_minmax2_np(d05, a, b, lane, mn, mx);
+        if (mn < lo) return true;
+        return mx > hi;
       };
       if (grp(ah, bh, hz(-60), hz(20))) isbad = true;
       else if (grp(a1, b1, hz(-60), hz(100))) isbad = true;
@@ -646,7 +648,7 @@ extern "C" __global__ __launch_bounds__(64) void ldg_k_hsync_lines(
         __syncthreads();
         const double high = np_mean(s_tmp, (int)(hi - lo));
         double zc2;
-        const int rc2 = wave_calczc(d05 + ah, wl, 0, (low + high) / 2, wl, lane, &zc2);
+        const int rc2 = wave_calczc_pf<3>(d05 + ah, wl, 0, (low + high) / 2, wl, lane, &zc2);
         if (rc2 != 0) { finish(v, 2); return; }   // None += ... -> TypeError
         zc2 += ((double)py_int(zc) - (fr * 1));
         if (fabs(zc2 - zc) < (fr / 4)) v = zc2;
@@ -716,16 +718,17 @@ extern "C" __global__ __launch_bounds__(256) void ldg_k_hsync_field(const int32_
 }
 
 // ---------------------------------------------------------------------------
-// Philips VBI decode (lddecode_core.py:814-884).  grid: n_reads x 64; lanes 0..2
-// decode one code line each, lane 0 then interprets them.
-extern "C" __global__ __launch_bounds__(64) void ldg_k_philips(
+// Philips VBI decode (lddecode_core.py:814-884).  grid: n_reads x 192; wave w
+// decodes code line w (decodephillipscode), thread 0 then interprets the three.
+// Each crossing search issues its loads at once (wave_calczc_pf), together with
+// the previous crossing's bit sample, so a crossing costs ~one memory latency.
+extern "C" __global__ __launch_bounds__(192) void ldg_k_philips(
     const int32_t* __restrict__ smap, const double* __restrict__ video, int64_t vread_stride, int64_t vchan_stride, SysConst C,
     FieldRec* __restrict__ recs, const double* __restrict__ lines) {
   prio_latency();
-
   __shared__ int32_t s_code[3][6];
   __shared__ int32_t s_ok[3];
-  const int lane = threadIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int slot = smap[blockIdx.x];
   FieldRec* R = recs + slot;
   if (R->status != FS_PENDING) return;
@@ -734,42 +737,41 @@ extern "C" __global__ __launch_bounds__(64) void ldg_k_philips(
   const double* L2 = lines + (int64_t)slot * LINES_STRIDE + LL2 * MAX_LINES;
   const double fr = C.freq;
   const double thr = C.ire0 + (C.hz_ire * 50);
-  if (lane < 3) {
+  {
     int ok = 0;
-    const int ln = C.codelines[lane];
+    const int ln = C.codelines[w];
     const double start = L2[ln];
     double cur;
-    int rc = calczc(dm, len, (double)py_int(start + 2 * fr), thr, py_int(12 * fr), &cur);
+    int rc = wave_calczc_pf<8>(dm, len, (double)py_int(start + 2 * fr), thr, py_int(12 * fr), lane, &cur);
     int n = 0;
-    int bits[24];
-    double first = 0, prevz = 0, gmin = __builtin_inf(), gmax = -__builtin_inf();
+    uint32_t bits = 0;                        // bit n at position 23 - n (n < 24)
+    double prevz = 0, gmin = __builtin_inf(), gmax = -__builtin_inf();
     bool crash = false;
     while (rc == 0) {
       int64_t bi;
       if (!py_index(py_int(cur - 0.5 * fr), len, bi)) { crash = true; break; }
-      if (n < 24) bits[n] = dm[bi] < thr ? 1 : 0;
+      const double vb = dm[bi];               // in flight with the next search's loads
       if (n > 0) {
         const double g = (cur - prevz) / fr;
         gmin = fmin(gmin, g); gmax = fmax(gmax, g);
-      } else {
-        first = cur;
       }
       prevz = cur;
+      const double c0 = cur;
+      if (n + 1 > 100000) { if (n < 24 && vb < thr) bits |= 1u << (23 - n); n++; break; }
+      rc = wave_calczc_pf<1>(dm, len, c0 + 1.9 * fr, thr, py_int(0.2 * fr), lane, &cur);
+      if (n < 24 && vb < thr) bits |= 1u << (23 - n);
       n++;
-      if (n > 100000) break;
-      rc = calczc(dm, len, cur + 1.9 * fr, thr, py_int(0.2 * fr), &cur);
     }
-    (void)first;
     if (rc < 0 || crash) ok = -1;
     else if (n == 24 && gmin > 1.85 && gmax < 2.15) {
       ok = 1;
-      for (int b = 0; b < 6; b++)
-        s_code[lane][b] = (bits[4 * b] << 3) | (bits[4 * b + 1] << 2) | (bits[4 * b + 2] << 1) | bits[4 * b + 3];
+      if (lane == 0)
+        for (int b = 0; b < 6; b++) s_code[w][b] = (int32_t)((bits >> (20 - 4 * b)) & 15u);
     }
-    s_ok[lane] = ok;
+    if (lane == 0) s_ok[w] = ok;
   }
   __syncthreads();
-  if (lane != 0) return;
+  if (tid != 0) return;
   for (int q = 0; q < 3; q++)
     if (s_ok[q] < 0) { R->status = FS_CRASH; return; }   // IndexError outside the reference's try
   int minutes = VBI_NONE, seconds = VBI_NONE, clvframe = VBI_NONE, framenr = VBI_NONE, statusv = VBI_NONE;

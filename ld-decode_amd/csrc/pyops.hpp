@@ -26,6 +26,24 @@ __device__ inline double pw_block(const double* a, int n) {
   return res;
 }
 
+// pw_block of a[0..n) (n <= 128) on one wave, result in every lane: lanes 0..7
+// run the eight accumulators, a shuffle tree combines them in numpy's order.
+__device__ inline double wave_pw_block(const double* a, int n, int lane) {
+  if (n < 8) return __shfl(lane == 0 ? pw_block(a, n) : 0.0, 0);
+  const int nb = n - (n % 8);
+  double r = 0.0;
+  if (lane < 8) {
+    r = a[lane];
+    for (int i = 8 + lane; i < nb; i += 8) r += a[i];
+  }
+  r = r + __shfl_xor(r, 1);
+  r = r + __shfl_xor(r, 2);
+  r = r + __shfl_xor(r, 4);
+  double res = __shfl(r, 0);
+  for (int i = nb; i < n; i++) res += a[i];
+  return res;
+}
+
 template <int L> __device__ inline double pw_sum_l(const double* a, int n) {
   if (n <= 128) return pw_block(a, n);
   int n2 = n / 2;
@@ -130,6 +148,47 @@ __device__ inline int wave_calczc(const double* data, int64_t len, double start_
   return 0;
 }
 
+// wave_calczc with every load of the search issued at once (the sample at the
+// start, up to 64 * MAXC window samples and their left neighbours), so the
+// search costs one memory latency instead of one per 64-sample chunk.  Windows
+// longer than 64 * MAXC samples, or a negative start, take wave_calczc.
+template <int MAXC>
+__device__ inline int wave_calczc_pf(const double* data, int64_t len, double start_offset, double target,
+                                     int64_t count, int lane, double* res) {
+  const int64_t s = py_int(start_offset);
+  const int64_t n = count + 1;
+  int64_t si;
+  if (!py_index(s, len, si)) return -1;
+  int64_t lo, hi;
+  py_slice(s, s + n, len, lo, hi);
+  if (s < 0 || hi - lo > 64 * MAXC) return wave_calczc(data, len, start_offset, target, count, lane, res);
+  const double v0 = data[si];
+  double v[MAXC], vp[MAXC];
+#pragma unroll
+  for (int c = 0; c < MAXC; c++) {
+    const int64_t k = lo + 64 * c + lane;
+    v[c] = (k < hi) ? data[k] : 0.0;
+    vp[c] = (k < hi && k >= 1) ? data[k - 1] : 0.0;
+  }
+  const bool rising = v0 < target;
+#pragma unroll
+  for (int c = 0; c < MAXC; c++) {
+    const int64_t k = lo + 64 * c + lane;
+    const bool p = k < hi && (rising ? (v[c] >= target) : (v[c] <= target));
+    const uint64_t m = __ballot(p);
+    if (m) {
+      const int h = __ffsll((unsigned long long)m) - 1;
+      const int64_t x = lo + 64 * c + h;           // lo == s here
+      if (x == 0) return 1;
+      const double a = __shfl(vp[c], h) - target;
+      const double b = __shfl(v[c], h) - target;
+      *res = (double)(x - 1) + ((-a) / ((-a) + b));
+      return 0;
+    }
+  }
+  return 1;
+}
+
 // np.min / np.max of data[a, b) (b > a): NaN if any element is NaN
 __device__ inline double wave_minmax_np(const double* data, int64_t a, int64_t b, bool is_max, int lane) {
   double m = is_max ? -__builtin_inf() : __builtin_inf();
@@ -144,6 +203,24 @@ __device__ inline double wave_minmax_np(const double* data, int64_t a, int64_t b
     m = is_max ? fmax(m, t) : fmin(m, t);
   }
   return __ballot(nan) ? __builtin_nan("") : m;
+}
+
+// np.min and np.max of data[a, b) (b > a) in one pass (each NaN if any element is NaN)
+__device__ inline void wave_minmax2_np(const double* data, int64_t a, int64_t b, int lane, double& mn, double& mx) {
+  double lo = __builtin_inf(), hi = -__builtin_inf();
+  bool nan = false;
+  for (int64_t k = a + lane; k < b; k += 64) {
+    const double v = data[k];
+    if (v != v) nan = true;
+    else { lo = fmin(lo, v); hi = fmax(hi, v); }
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    lo = fmin(lo, __shfl_xor(lo, o));
+    hi = fmax(hi, __shfl_xor(hi, o));
+  }
+  const bool any_nan = __ballot(nan) != 0;
+  mn = any_nan ? __builtin_nan("") : lo;
+  mx = any_nan ? __builtin_nan("") : hi;
 }
 
 // Sorted-window median helper: median of a[0..n) already sorted ascending.
@@ -234,3 +311,80 @@ __device__ inline void block_bitonic_sort(double* a, int npow2, int tid, int nth
 }
 
 }  // namespace ldg
+
+// ---- selection over doubles of any sign (no NaNs) ------------------------------
+// order-preserving unsigned key of a double (negative values bit-inverted)
+__device__ inline uint64_t dkey(double x) {
+  const uint64_t u = (uint64_t)__double_as_longlong(x);
+  return (u >> 63) ? ~u : (u | (1ull << 63));
+}
+__device__ inline double dkey_val(uint64_t k) {
+  const uint64_t u = (k >> 63) ? (k & ~(1ull << 63)) : ~k;
+  return __longlong_as_double((long long)u);
+}
+
+// k-th smallest key (0-based) of dkey(a[0..n)), one wave: radix select, 8 bits
+// per pass.  hist: 256 ints of LDS.
+__device__ inline uint64_t wave_kth_key(const double* a, int n, int k, int lane, int* hist) {
+  uint64_t prefix = 0, mask = 0;
+  for (int shift = 56; shift >= 0; shift -= 8) {
+    for (int d = lane; d < 256; d += 64) hist[d] = 0;
+    __syncthreads();
+    for (int i = lane; i < n; i += 64) {
+      const uint64_t u = dkey(a[i]);
+      if ((u & mask) == prefix) atomicAdd(&hist[(u >> shift) & 255], 1);
+    }
+    __syncthreads();
+    int c[4], tot = 0;
+#pragma unroll
+    for (int e = 0; e < 4; e++) { c[e] = hist[4 * lane + e]; tot += c[e]; }
+    int incl = tot;
+    for (int o = 1; o < 64; o <<= 1) {
+      const int v = __shfl_up(incl, o);
+      if (lane >= o) incl += v;
+    }
+    const int excl = incl - tot;
+    int digit = -1, below = 0;
+    if (k >= excl && k < incl) {
+      int run = excl;
+#pragma unroll
+      for (int e = 0; e < 4; e++) {
+        if (digit < 0 && k < run + c[e]) { digit = 4 * lane + e; below = run; }
+        run += c[e];
+      }
+    }
+    const uint64_t m = __ballot(digit >= 0);
+    const int src = __ffsll((unsigned long long)m) - 1;
+    digit = __shfl(digit, src);
+    below = __shfl(below, src);
+    k -= below;
+    prefix |= (uint64_t)digit << shift;
+    mask |= (uint64_t)255 << shift;
+    __syncthreads();
+  }
+  return prefix;
+}
+
+// np.median of a[0..n) (n > 0, no NaNs), one wave: the middle order statistic(s)
+// -- the value np.sort would put there (up to the sign of a zero).
+__device__ inline double wave_median(const double* a, int n, int lane, int* hist) {
+  if (n & 1) return dkey_val(wave_kth_key(a, n, n / 2, lane, hist));
+  const uint64_t k0 = wave_kth_key(a, n, n / 2 - 1, lane, hist);
+  // the next order statistic: k0 again if it occurs beyond rank n/2 - 1, else
+  // the smallest key above k0
+  int le = 0;
+  uint64_t up = ~0ull;
+  for (int i = lane; i < n; i += 64) {
+    const uint64_t u = dkey(a[i]);
+    if (u <= k0) le++;
+    else if (u < up) up = u;
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    le += __shfl_xor(le, o);
+    const uint64_t t = (uint64_t)__shfl_xor((long long)up, o);
+    up = t < up ? t : up;
+  }
+  const uint64_t k1 = (le >= n / 2 + 1) ? k0 : up;
+  return (dkey_val(k0) + dkey_val(k1)) / 2.0;
+}
+

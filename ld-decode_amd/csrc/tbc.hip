@@ -224,7 +224,7 @@ extern "C" __global__ __launch_bounds__(64) void ldg_k_burst_lines(
 
   // window rows for 40 outputs: <= 40 * SPL_MAXN / W + 2 * KTR + 4 < 384
   __shared__ SplineLDS<64, 384> S;
-  __shared__ double s_ba[40], s_t[40], s_g[2][40];
+  __shared__ double s_ba[40], s_t[40], s_g[2][40], s_zc[40];
   const int lane = threadIdx.x;
   const int slot = smap[blockIdx.x / MAX_LINES];
   const int l = blockIdx.x % MAX_LINES;
@@ -245,26 +245,43 @@ extern "C" __global__ __launch_bounds__(64) void ldg_k_burst_lines(
   const double b0 = li[l], b1 = li[l + 1];
   const double wow = (b1 - b0) / (double)C.linelen;
   const int W = C.outlinelen;
-  const int rc = spline_block<64>(bur, R->n_out, b0, b1, W, 20, 60, lane, S,
+  const int rc = spline_block<64, 4>(bur, R->n_out, b0, b1, W, 20, 60, lane, S,
                                   [&](int o, double v) { s_ba[o - 20] = v * wow; });
   if (rc < 0) {
     if (lane == 0) R->status = FS_TBC;   // benign race: every writer stores the same value
     return;
   }
   __syncthreads();
-  if (lane != 0) return;
+  // the burst statistics on the whole wave (numpy's pairwise sums via wave_pw_block)
   double* ba = s_ba;
   double* tt = s_t;
   const double hzs = 1700000 / 140.0;
-  const double m = pw_sum(ba, 40) / 40.0;
-  double mx = 0.0;
-  for (int i = 0; i < 40; i++) { const double v = ba[i] - m; ba[i] = v; mx = fmax(mx, fabs(v)); }
+  const double m = (0.0 + wave_pw_block(ba, 40, lane)) / 40.0;
+  double v = 0.0, amx = 0.0;
+  if (lane < 40) { v = ba[lane] - m; amx = fabs(v); }
+  for (int o = 32; o > 0; o >>= 1) amx = fmax(amx, __shfl_xor(amx, o));   // fmax drops NaNs, as the loop did
+  const double mx = fmax(0.0, amx);
+  __syncthreads();
+  if (lane < 40) ba[lane] = v;
+  __syncthreads();
   const float lf = (float)mx;
   const double lv = (double)lf;               // numpy-1: float32 element promoted to float64
   // np.std(ba)
-  const double m2 = pw_sum(ba, 40) / 40.0;
-  for (int i = 0; i < 40; i++) { const double d = ba[i] - m2; tt[i] = d * d; }
-  const double sd = sqrt(pw_sum(tt, 40) / 40.0);
+  const double m2 = (0.0 + wave_pw_block(ba, 40, lane)) / 40.0;
+  if (lane < 40) { const double d = ba[lane] - m2; tt[lane] = d * d; }
+  __syncthreads();
+  const double sd = sqrt((0.0 + wave_pw_block(tt, 40, lane)) / 40.0);
+  // every start position's crossing (calczc over <= 11 samples), one lane each;
+  // lane 0 then walks them in the reference's order
+  if (lane < 40) {
+    s_zc[lane] = -1.0;
+    if (fabs(ba[lane]) > lv * .6) {
+      double zc;
+      if (calczc_s(ba, 40, lane, 0.0, 10, 1, &zc) == 0) s_zc[lane] = zc;
+    }
+  }
+  __syncthreads();
+  if (lane != 0) return;
   double p0 = 0.0, p1 = 0.0;
   float out_level = lf;
   if (((lv / hzs) > 30) || (sd / hzs) < 3) {
@@ -275,17 +292,15 @@ extern "C" __global__ __launch_bounds__(64) void ldg_k_burst_lines(
     int cnt = 0, nF = 0, nT = 0;
     int bi = 0;
     while (bi < 40) {
-      if (fabs(ba[bi]) > lv * .6) {
-        double zc;
-        if (calczc_s(ba, 40, bi, 0.0, 10, 1, &zc) == 0) {
-          double off = zc - ((floor(zc / 4) * 4) - 1);
-          if (off > 3.5) off -= 4;
-          const bool pos = ba[bi] > 0;
-          tt[cnt] = off;
-          if (pos) { tag |= (1ull << cnt); nT++; } else nF++;
-          cnt++;
-          bi = (int)zc;
-        }
+      const double zc = s_zc[bi];             // >= 0: this start qualifies and has a crossing
+      if (zc >= 0.0) {
+        double off = zc - ((floor(zc / 4) * 4) - 1);
+        if (off > 3.5) off -= 4;
+        const bool pos = ba[bi] > 0;
+        tt[cnt] = off;
+        if (pos) { tag |= (1ull << cnt); nT++; } else nF++;
+        cnt++;
+        bi = (int)zc;
       }
       bi += 1;
     }
@@ -307,6 +322,9 @@ extern "C" __global__ __launch_bounds__(64) void ldg_k_burst_lines(
   lvl[l] = out_level;
   pv0[l] = p0;
   pv1[l] = p1;
+#ifdef LDG_STAMPS
+  if (blockIdx.x < KST_BLOCKS) g_kst[4][blockIdx.x][7] = __builtin_readcyclecounter();
+#endif
 }
 
 // Per-read part of refine_linelocs_burst (lddecode_core.py:1112-1133) and, on
@@ -319,7 +337,10 @@ extern "C" __global__ __launch_bounds__(64) void ldg_k_burst_field(const int32_t
   prio_latency();
 
   __shared__ double s_c0[512], s_c1[512];
-  __shared__ int s_nc;
+  __shared__ int s_hist[256];
+  __shared__ double s_lo[MAX_LINES];
+  __shared__ float s_lvl[MAX_LINES];
+  __shared__ int s_g;
   const int lane = threadIdx.x;
   const int slot = smap[blockIdx.x];
   FieldRec* R = recs + slot;
@@ -331,49 +352,79 @@ extern "C" __global__ __launch_bounds__(64) void ldg_k_burst_field(const int32_t
   const double* pv0 = LN + PAVG0 * MAX_LINES;
   const double* pv1 = LN + PAVG1 * MAX_LINES;
   float* lvl = blevel + (int64_t)slot * MAX_LINES;
-  // phaseaverages_cut: rows with a nonzero entry, then np.median of each column (wave bitonic sort)
-  if (lane == 0) {
-    int nc = 0;
-    for (int l = 0; l < nl; l++)
-      if (pv0[l] != 0 || pv1[l] != 0) { s_c0[nc] = pv0[l]; s_c1[nc] = pv1[l]; nc++; }
-    s_nc = nc;
+  KSTAMP(2, 0);
+  // phaseaverages_cut: rows with a nonzero entry (NaN counts as nonzero), in
+  // order -- a ballot compaction -- then np.median of each column (wave bitonic sort)
+  int nc = 0;
+  for (int l0 = 0; l0 < nl; l0 += 64) {
+    const int l = l0 + lane;
+    double a0 = 0.0, a1 = 0.0;
+    bool p = false;
+    if (l < nl) { a0 = pv0[l]; a1 = pv1[l]; p = (a0 != 0 || a1 != 0); }
+    const uint64_t m = __ballot(p);
+    if (p) {
+      const int pos = nc + __popcll(m & ((1ull << lane) - 1));
+      s_c0[pos] = a0;
+      s_c1[pos] = a1;
+    }
+    nc += __popcll(m);
   }
-  __syncthreads();
-  const int nc = s_nc;
-  int np2 = 1;
-  while (np2 < nc) np2 <<= 1;
-  for (int k = nc + lane; k < np2; k += 64) { s_c0[k] = __builtin_inf(); s_c1[k] = __builtin_inf(); }
   __syncthreads();
   bool nan0 = false, nan1 = false;
   for (int k = lane; k < nc; k += 64) { nan0 |= s_c0[k] != s_c0[k]; nan1 |= s_c1[k] != s_c1[k]; }
   nan0 = __any(nan0);
   nan1 = __any(nan1);
-  if (nc > 1) {
-    block_bitonic_sort(s_c0, np2, lane, 64);
-    block_bitonic_sort(s_c1, np2, lane, 64);
-  }
-  if (lane != 0) return;
-  const double m0 = nan0 ? __builtin_nan("") : sorted_median(s_c0, nc);
-  const double m1 = nan1 ? __builtin_nan("") : sorted_median(s_c1, nc);
-  const int g = (fabs(m0) < fabs(m1)) ? 0 : 1;
+  KSTAMP(2, 1);
+  // np.median of each column (NaN if the column has one), by radix select
+  const double m0 = (nan0 || nc == 0) ? __builtin_nan("") : wave_median(s_c0, nc, lane, s_hist);
+  const double m1 = (nan1 || nc == 0) ? __builtin_nan("") : wave_median(s_c1, nc, lane, s_hist);
+  KSTAMP(2, 2);
+  if (lane == 0) s_g = (fabs(m0) < fabs(m1)) ? 0 : 1;
+  __syncthreads();
+  const int g = s_g;
   const double* adj = g ? pv1 : pv0;
-  for (int l = g; l < nl; l += 2) lvl[l] = -lvl[l];
   const double K = C.freq / ((4.0 * 315.0) / 88.0);
-  for (int l = 0; l < nl; l++) {
+  // the group's lines flip their level sign; a phase adjustment beyond 2 samples
+  // zeroes the level, otherwise it moves the line (lddecode_core.py:1120-1127)
+  for (int l = lane; l < nl; l += 64) {
+    float lv = lvl[l];
+    if ((l & 1) == g) lv = -lv;
     double v = li[l];
-    if (fabs(adj[l]) > 2) lvl[l] = 0.0f;
-    else v -= adj[l] * K * 1;
-    lo[l] = v;
+    const double a = adj[l];
+    if (fabs(a) > 2) lv = 0.0f;
+    else v -= a * K * 1;
+    s_lo[l] = v;
+    s_lvl[l] = lv;
   }
-  for (int l = 2; l < nl - 1; l++)
-    if (lvl[l] == 0.0f) lo[l] = (lo[l - 1] + lo[l + 1]) / 2;
-  R->burst_group = g;
-  if (pass == 1) {
-    const double shift = (90 + 1.5) * (3.141592653589793 / 180);
-    const double c = (shift - 8) * K;
-    double* lf = LN + LLF * MAX_LINES;
-    for (int l = 0; l < nl; l++) lf[l] = (lo[l] + 0) + c;
+  __syncthreads();
+  // lines with no burst take the mean of their neighbours, in line order (a
+  // line's left neighbour may itself have just been replaced): lane 0 visits
+  // only those lines, found by ballot
+  for (int l0 = 2; l0 < nl - 1; l0 += 64) {
+    const int l = l0 + lane;
+    const uint64_t m = __ballot(l < nl - 1 && s_lvl[l] == 0.0f);
+    if (lane == 0) {
+      uint64_t mm = m;
+      while (mm) {
+        const int j = l0 + __ffsll((unsigned long long)mm) - 1;
+        mm &= mm - 1;
+        s_lo[j] = (s_lo[j - 1] + s_lo[j + 1]) / 2;
+      }
+    }
+    __syncthreads();
   }
+  const double shift = (90 + 1.5) * (3.141592653589793 / 180);
+  const double c = (shift - 8) * K;
+  double* lf = LN + LLF * MAX_LINES;
+  for (int l = lane; l < nl; l += 64) {
+    lo[l] = s_lo[l];
+    lvl[l] = s_lvl[l];
+    if (pass == 1) lf[l] = (s_lo[l] + 0) + c;
+  }
+  if (lane == 0) R->burst_group = g;
+#ifdef LDG_STAMPS
+  if (blockIdx.x < KST_BLOCKS) g_kst[2][blockIdx.x][3] = __builtin_readcyclecounter();
+#endif
 }
 
 // Final resample of 'demod' (lineoffset 1 NTSC / 3 PAL, wow) to uint16 .tbc
