@@ -98,7 +98,7 @@ __device__ __forceinline__ double block_affine_carry(double A, double B, bool su
   return c;
 }
 
-template <int NT, int STK = -1, class SL, class Sink>
+template <int NT, int STK = -1, bool PRELOADED = false, class SL, class Sink>
 __device__ int spline_block(const double* __restrict__ buf, int64_t len, double begin, double end, int W, int o_lo,
                             int o_hi, int tid, SL& S, Sink&& sink) {
   if constexpr (STK >= 0) KSTAMP(STK, 0);
@@ -124,10 +124,19 @@ __device__ int spline_block(const double* __restrict__ buf, int64_t len, double 
   if (top - base + 1 > SL::cap) return -1;                    // unreachable for n < SPL_MAXN (see callers)
   double* ys = S.ys - base;
   double* ms = S.ms - base;
-  for (int j = base + tid; j <= top; j += NT) ys[j] = y[j];
-  if (tid == 0) {
-    S.m1 = (6.0 * ((y[2] - y[1]) - (y[1] - y[0]))) / 6.0;
-    S.mn1 = (6.0 * ((y[n] - y[n - 1]) - (y[n - 1] - y[n - 2]))) / 6.0;
+  if constexpr (PRELOADED) {
+    // the caller staged y[0..n] in S.ys (base == 0 for a whole-line solve)
+    __syncthreads();
+    if (tid == 0) {
+      S.m1 = (6.0 * ((ys[2] - ys[1]) - (ys[1] - ys[0]))) / 6.0;
+      S.mn1 = (6.0 * ((ys[n] - ys[n - 1]) - (ys[n - 1] - ys[n - 2]))) / 6.0;
+    }
+  } else {
+    for (int j = base + tid; j <= top; j += NT) ys[j] = y[j];
+    if (tid == 0) {
+      S.m1 = (6.0 * ((y[2] - y[1]) - (y[1] - y[0]))) / 6.0;
+      S.mn1 = (6.0 * ((y[n] - y[n - 1]) - (y[n - 1] - y[n - 2]))) / 6.0;
+    }
   }
   __syncthreads();
   if constexpr (STK >= 0) KSTAMP(STK, 1);
@@ -137,43 +146,63 @@ __device__ int spline_block(const double* __restrict__ buf, int64_t len, double 
   int CH = (T + NT - 1) / NT;
   CH |= 1;
   const int t0 = tid * CH;
-  const int t1 = (t0 + CH < T) ? t0 + CH : T;
+  const int nq = ((t0 + CH < T) ? t0 + CH : T) - t0;         // this thread's rows (may be <= 0)
   auto ct = [&](int t) { return S.ct[t < 16 ? t : 16]; };
-  auto rhs = [&](int t) {
-    const int j = lo + t;
-    double r = 6.0 * ((ys[j + 1] - ys[j]) - (ys[j] - ys[j - 1]));
-    if (t == 0) r -= BL;
-    if (t == T - 1) r -= BR;
-    return r;
-  };
+  // the thread's right-hand sides and Thomas coefficients, all loaded up front
+  // (CHMAX >= CH: the loops are unrolled and predicated, so the LDS reads issue together)
+  constexpr int CHMAX = ((SL::cap + NT - 1) / NT) | 1;
+  double rr[CHMAX], cc[CHMAX], dd[CHMAX];
+#pragma unroll
+  for (int q = 0; q < CHMAX; q++) {
+    if (q < nq) {
+      const int t = t0 + q, j = lo + t;
+      double r = 6.0 * ((ys[j + 1] - ys[j]) - (ys[j] - ys[j - 1]));
+      if (t == 0) r -= BL;
+      if (t == T - 1) r -= BR;
+      rr[q] = r;
+      cc[q] = ct(t);
+    }
+  }
   // forward sweep: d -> -c d + c r
   double A = 1.0, B = 0.0;
-  for (int t = t0; t < t1; t++) {
-    const double c = ct(t);
-    A = -c * A;
-    B = (rhs(t) - B) * c;
+#pragma unroll
+  for (int q = 0; q < CHMAX; q++) {
+    if (q < nq) {
+      const double c = cc[q];
+      A = -c * A;
+      B = (rr[q] - B) * c;
+    }
   }
   double dprev = block_affine_carry<NT>(A, B, false, tid, S);
   if constexpr (STK >= 0) KSTAMP(STK, 2);
-  for (int t = t0; t < t1; t++) {
-    const double d = (rhs(t) - dprev) * ct(t);
-    ms[lo + t] = d;
-    dprev = d;
+#pragma unroll
+  for (int q = 0; q < CHMAX; q++) {
+    if (q < nq) {
+      const double d = (rr[q] - dprev) * cc[q];
+      dd[q] = d;
+      dprev = d;
+    }
   }
   // back substitution: M -> d - c M, top down
   A = 1.0; B = 0.0;
-  for (int t = t1 - 1; t >= t0; t--) {
-    const double c = ct(t);
-    A = -c * A;
-    B = ms[lo + t] - c * B;
+#pragma unroll
+  for (int q = CHMAX - 1; q >= 0; q--) {
+    if (q < nq) {
+      const double c = cc[q];
+      A = -c * A;
+      B = dd[q] - c * B;
+    }
   }
   if constexpr (STK >= 0) KSTAMP(STK, 3);
   double Mnext = block_affine_carry<NT>(A, B, true, tid, S);
   if constexpr (STK >= 0) KSTAMP(STK, 4);
-  for (int t = t1 - 1; t >= t0; t--) {
-    const double M = ms[lo + t] - ct(t) * Mnext;
-    ms[lo + t] = M;
-    Mnext = M;
+#pragma unroll
+  for (int q = CHMAX - 1; q >= 0; q--) {
+    if (q < nq) {
+      const double M = dd[q] - cc[q] * Mnext;
+      ms[lo + t0 + q] = M;
+      Mnext = M;
+    }
   }
   __syncthreads();
   if (tid == 0) {
@@ -224,7 +253,7 @@ extern "C" __global__ __launch_bounds__(64) void ldg_k_burst_lines(
 
   // window rows for 40 outputs: <= 40 * SPL_MAXN / W + 2 * KTR + 4 < 384
   __shared__ SplineLDS<64, 384> S;
-  __shared__ double s_ba[40], s_t[40], s_g[2][40], s_zc[40];
+  __shared__ double s_ba[40], s_t[40], s_g[2][40];
   const int lane = threadIdx.x;
   const int slot = smap[blockIdx.x / MAX_LINES];
   const int l = blockIdx.x % MAX_LINES;
@@ -271,53 +300,47 @@ extern "C" __global__ __launch_bounds__(64) void ldg_k_burst_lines(
   if (lane < 40) { const double d = ba[lane] - m2; tt[lane] = d * d; }
   __syncthreads();
   const double sd = sqrt((0.0 + wave_pw_block(tt, 40, lane)) / 40.0);
-  // every start position's crossing (calczc over <= 11 samples), one lane each;
-  // lane 0 then walks them in the reference's order
-  if (lane < 40) {
-    s_zc[lane] = -1.0;
-    if (fabs(ba[lane]) > lv * .6) {
-      double zc;
-      if (calczc_s(ba, 40, lane, 0.0, 10, 1, &zc) == 0) s_zc[lane] = zc;
-    }
+  // the zero-crossing walk (lddecode_core.py:1089-1104): every start position's
+  // crossing (calczc over <= 11 samples) on its own lane; the walk from 0 visits
+  // the first qualifying position at or after the previous one's int(zc) + 1,
+  // so it reduces to bit scans over the qualifying mask (v_readlane for the jumps)
+  bool qual = false;
+  double zc = 0.0;
+  if (lane < 40 && fabs(ba[lane]) > lv * .6) qual = calczc_s(ba, 40, lane, 0.0, 10, 1, &zc) == 0;
+  const bool pos = lane < 40 && ba[lane] > 0;
+  double off = 0.0;
+  if (qual) {
+    off = zc - ((floor(zc / 4) * 4) - 1);
+    if (off > 3.5) off -= 4;
   }
+  const uint64_t Q = __ballot(qual), P = __ballot(qual && pos);
+  const int jt = qual ? (int)zc + 1 : 0;
+  uint64_t V = 0;
+  for (int x = 0; x < 40;) {
+    const uint64_t m = Q & (~0ull << x);
+    if (!m) break;
+    const int q = __ffsll((unsigned long long)m) - 1;
+    V |= 1ull << q;
+    x = __builtin_amdgcn_readlane(jt, q);
+  }
+  const uint64_t VT = V & P, VF = V & ~P;
+  const int nT = __popcll(VT), nF = __popcll(VF);
+  // each group's offsets in visiting (= position) order
+  const uint64_t below = (1ull << lane) - 1;
+  if ((VT >> lane) & 1) s_g[1][__popcll(VT & below)] = off;
+  if ((VF >> lane) & 1) s_g[0][__popcll(VF & below)] = off;
   __syncthreads();
   if (lane != 0) return;
   double p0 = 0.0, p1 = 0.0;
   float out_level = lf;
   if (((lv / hzs) > 30) || (sd / hzs) < 3) {
     out_level = 0.0f;
-  } else {
-    // zero crossings: offsets stored in tt (in order), group in a bit mask
-    uint64_t tag = 0;
-    int cnt = 0, nF = 0, nT = 0;
-    int bi = 0;
-    while (bi < 40) {
-      const double zc = s_zc[bi];             // >= 0: this start qualifies and has a crossing
-      if (zc >= 0.0) {
-        double off = zc - ((floor(zc / 4) * 4) - 1);
-        if (off > 3.5) off -= 4;
-        const bool pos = ba[bi] > 0;
-        tt[cnt] = off;
-        if (pos) { tag |= (1ull << cnt); nT++; } else nF++;
-        cnt++;
-        bi = (int)zc;
-      }
-      bi += 1;
-    }
-    if (!(nF < 3 || nT < 3)) {
-      // mean of each group's [1:-1] (np.array of the list, pairwise sum)
-      double* gF = s_g[0];
-      double* gT = s_g[1];
-      int kF = 0, kT = 0;
-      for (int k = 0; k < cnt; k++) {
-        if ((tag >> k) & 1) gT[kT++] = tt[k];
-        else gF[kF++] = tt[k];
-      }
-      const double mF = pw_sum(gF + 1, kF - 2) / (double)(kF - 2);
-      const double mT = pw_sum(gT + 1, kT - 2) / (double)(kT - 2);
-      if (l % 2) { p0 = 2 - mT; p1 = 2 - mF; }
-      else { p0 = 2 - mF; p1 = 2 - mT; }
-    }
+  } else if (!(nF < 3 || nT < 3)) {
+    // mean of each group's [1:-1] (np.array of the list, pairwise sum)
+    const double mF = pw_sum(s_g[0] + 1, nF - 2) / (double)(nF - 2);
+    const double mT = pw_sum(s_g[1] + 1, nT - 2) / (double)(nT - 2);
+    if (l % 2) { p0 = 2 - mT; p1 = 2 - mF; }
+    else { p0 = 2 - mF; p1 = 2 - mT; }
   }
   lvl[l] = out_level;
   pv0[l] = p0;
@@ -429,53 +452,92 @@ extern "C" __global__ __launch_bounds__(64) void ldg_k_burst_field(const int32_t
 
 // Final resample of 'demod' (lineoffset 1 NTSC / 3 PAL, wow) to uint16 .tbc
 // lines (lddecode_core.py:1135-1159 NTSC, :1023-1035 PAL).
-// grid: n_reads * LINE_GROUPS workgroups of 64 threads; lane = output row.
+// grid: n_reads * FINAL_GROUPS workgroups of FINAL_NT threads; a workgroup
+// resamples FINAL_LPW consecutive lines, loading the next line's samples into
+// registers while it solves the current one (the loads are off the critical path).
 constexpr int FINAL_NT = 256;
+constexpr int FINAL_LPW = 4;
+constexpr int FINAL_GROUPS = MAX_LINES / FINAL_LPW;
+constexpr int FINAL_PF = (SPL_MAXN + FINAL_NT - 1) / FINAL_NT;     // samples per thread per line
 extern "C" __global__ __launch_bounds__(FINAL_NT) void ldg_k_final_lines(
     const int32_t* __restrict__ smap, const double* __restrict__ video, int64_t vread_stride, int64_t vchan_stride,
     SysConst C, FieldRec* __restrict__ recs, const double* __restrict__ lines, const float* __restrict__ blevel,
     uint16_t* __restrict__ pic, int64_t pic_stride) {
   prio_latency();
-
   __shared__ SplineLDS<FINAL_NT> S;
   const int tid = threadIdx.x;
-  const int slot = smap[blockIdx.x / MAX_LINES];
-  const int row = blockIdx.x % MAX_LINES;
+  const int slot = smap[blockIdx.x / FINAL_GROUPS];
+  const int row0 = (blockIdx.x % FINAL_GROUPS) * FINAL_LPW;
   FieldRec* R = recs + slot;
   if (R->status != FS_PENDING) return;
   const int lc = R->linecount;
-  if (row >= lc) return;
+  if (row0 >= lc) return;
+  const int row1 = (row0 + FINAL_LPW < lc) ? row0 + FINAL_LPW : lc;
   const int loff = (C.system == 1) ? 3 : 1;
-  const int l = row + loff;
   const double* lf = lines + (int64_t)slot * LINES_STRIDE + LLF * MAX_LINES;
   const double* dm = video + (int64_t)slot * vread_stride + (int64_t)CH_DEMOD * vchan_stride;
+  const int64_t len = R->n_out;
   const int W = C.outlinelen;
-  uint16_t* out = pic + (int64_t)slot * pic_stride + (int64_t)row * W;
-  const double b0 = lf[l], b1 = lf[l + 1];
-  const double wow = (b1 - b0) / (double)C.linelen;
   const bool pal = C.system == 1;
   const double scale_ = pal ? (double)(0xd300 - 0x0100) / (100 - C.vsync_ire)
                             : (double)(0xc800 - 0x0400) / (100 - C.vsync_ire);
   const double base = pal ? 256.0 : 1024.0;
-  const int rc = spline_block<FINAL_NT, 1>(dm, R->n_out, b0, b1, W, 0, W, tid, S, [&](int o, double v) {
-    double red = ((v * wow) - C.ire0) / C.hz_ire;
-    red -= C.vsync_ire;
-    double x = (red * scale_) + base;
-    if (x != x) x = 0.0;
-    x = fmin(fmax(x, 0.0), 65535.0) + 0.5;
-    out[o] = (uint16_t)x;
-  });
-  if (rc < 0) {
-    if (tid == 0) R->status = FS_TBC;
-    return;
-  }
-  // NTSC burst flag pixels (threads 0 / 1 wrote pixels 0 / 1 above)
-  if (!pal && tid < 2 && row >= 1 && row < lc - 1) {
-    const float bl = blevel[(int64_t)slot * MAX_LINES + row];
-    const double hzs = 1700000 / 140.0;
-    if (tid == 0) out[0] = bl > 0 ? 16384 : 32768;
-    const double clevel = (1 / 1.45) / hzs;
-    if (tid == 1) out[1] = (uint16_t)(327.67 * clevel * fabs((double)bl));
+  // line geometry as spline_block checks it: samples y[0..n] = dm[ib .. ib + n]
+  auto geom = [&](int row, int64_t& ib, int& n) {
+    const int64_t b = py_int(lf[row + loff]), e = py_int(lf[row + loff + 1]);
+    const int64_t n64 = e - b;
+    ib = b;
+    n = (b < 0 || n64 < 6 || n64 >= SPL_MAXN || b + n64 + 1 > len) ? -1 : (int)n64;
+  };
+  double pre[FINAL_PF];
+  auto prefetch = [&](int row) {
+    int64_t ib;
+    int n;
+    geom(row, ib, n);
+#pragma unroll
+    for (int q = 0; q < FINAL_PF; q++) {
+      const int j = tid + FINAL_NT * q;
+      pre[q] = (j <= n) ? dm[ib + j] : 0.0;
+    }
+  };
+  prefetch(row0);
+  for (int row = row0; row < row1; row++) {
+    int64_t ib;
+    int n;
+    geom(row, ib, n);
+    __syncthreads();                           // the previous line's evaluation is done with S
+    if (n > 0) {
+#pragma unroll
+      for (int q = 0; q < FINAL_PF; q++) {
+        const int j = tid + FINAL_NT * q;
+        if (j <= n) S.ys[j] = pre[q];
+      }
+    }
+    if (row + 1 < row1) prefetch(row + 1);
+    const int l = row + loff;
+    uint16_t* out = pic + (int64_t)slot * pic_stride + (int64_t)row * W;
+    const double b0 = lf[l], b1 = lf[l + 1];
+    const double wow = (b1 - b0) / (double)C.linelen;
+    const int rc = spline_block<FINAL_NT, 1, true>(dm, len, b0, b1, W, 0, W, tid, S, [&](int o, double v) {
+      double red = ((v * wow) - C.ire0) / C.hz_ire;
+      red -= C.vsync_ire;
+      double x = (red * scale_) + base;
+      if (x != x) x = 0.0;
+      x = fmin(fmax(x, 0.0), 65535.0) + 0.5;
+      out[o] = (uint16_t)x;
+    });
+    if (rc < 0) {
+      if (tid == 0) R->status = FS_TBC;
+      return;                                  // uniform: rc depends only on the line geometry
+    }
+    // NTSC burst flag pixels (threads 0 / 1 wrote pixels 0 / 1 above)
+    if (!pal && tid < 2 && row >= 1 && row < lc - 1) {
+      const float bl = blevel[(int64_t)slot * MAX_LINES + row];
+      const double hzs = 1700000 / 140.0;
+      if (tid == 0) out[0] = bl > 0 ? 16384 : 32768;
+      const double clevel = (1 / 1.45) / hzs;
+      if (tid == 1) out[1] = (uint16_t)(327.67 * clevel * fabs((double)bl));
+    }
   }
 }
 
