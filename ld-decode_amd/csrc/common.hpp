@@ -76,6 +76,25 @@ struct SysConst {
   int32_t pad_;
 };
 
+// Sync-channel tiles: for every 32 consecutive demod_sync outputs of a read
+// (tile t = outputs [32 t, 32 t + 32); overlap-save blocks keep 15328 = 32 * 479
+// outputs, so a tile never straddles two blocks) the maximum and the index of
+// its first occurrence, np.argmax order (a NaN is the maximum, the first NaN
+// wins).  The demod writes them beside the channel; get_syncpeaks' window
+// argmax then reads whole tiles plus the two ragged ends.
+struct SyncTile {
+  double v;
+  int64_t idx;             // absolute output index (INT64_MAX: tile has no output)
+};
+constexpr int64_t STILE_PER_SLOT = MAX_NOUT / 32 + 2;
+
+// (v, vi) comes before (b, bi) in np.argmax order
+__device__ __forceinline__ bool am_beats(double v, int64_t vi, double b, int64_t bi) {
+  const bool vn = v != v, bn = b != b;
+  if (vn || bn) return vn && (!bn || vi < bi);
+  return v > b || (v == b && vi < bi);
+}
+
 // Latency-bound kernels (a wave per read / per line, one lane per recurrence)
 // share CUs with the FP64-throughput demod; raise their wave priority so the
 // SIMD arbiter issues their serial chains first (demod waves fill the gaps).

@@ -196,7 +196,7 @@ extern "C" __global__ __launch_bounds__(1024) void ldg_k_demod(
     const double2* __restrict__ a_lfilt, const double2* __restrict__ a_rfilt, SysConst C,
     double* __restrict__ video, int64_t vread_stride, int64_t vchan_stride,
     double* __restrict__ audio1, int64_t aread_stride, int64_t achan_stride, int32_t* __restrict__ status,
-    double2* __restrict__ ospill) {
+    double2* __restrict__ ospill, SyncTile* __restrict__ stiles) {
   __shared__ double2 s_x[M];          // 128 KiB: the 8192-point transforms
   __shared__ double2 s_a[2048];       // 32 KiB: the two 1024-point audio transforms
   const CBuf X_{s_x}, A_{s_a};
@@ -413,6 +413,26 @@ extern "C" __global__ __launch_bounds__(1024) void ldg_k_demod(
         if (in0 && in1) *reinterpret_cast<double2*>(o + p) = make_double2(z.x * inv, z.y * inv);
         else if (in0) o[p] = z.x * inv;
         else if (in1) o[p + 1] = z.y * inv;
+        if (kind == 4) {
+          // sync tile of outputs [p & ~31, +32): 16 lanes, np.argmax order
+          const int64_t n0 = (int64_t)off + p - BLOCKCUT;
+          double v = -__builtin_inf();
+          int64_t vi = 0x7fffffffffffffffLL;
+          if (in0) { v = z.x * inv; vi = n0; }
+          if (in1 && am_beats(z.y * inv, n0 + 1, v, vi)) { v = z.y * inv; vi = n0 + 1; }
+#pragma unroll
+          for (int o2 = 1; o2 < 16; o2 <<= 1) {
+            const double ov = __shfl_xor(v, o2);
+            const int64_t oi = __shfl_xor(vi, o2);
+            if (am_beats(ov, oi, v, vi)) { v = ov; vi = oi; }
+          }
+          if ((t & 15) == 0 && p >= BLOCKCUT && p < BLOCKCUT + copylen) {
+            SyncTile tt;
+            tt.v = v;
+            tt.idx = vi;
+            stiles[(int64_t)slot * STILE_PER_SLOT + (n0 >> 5)] = tt;
+          }
+        }
       }
       __syncthreads();
     } else {

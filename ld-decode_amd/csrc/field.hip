@@ -47,11 +47,6 @@ struct SyncView {
 // maximum; the first NaN wins), one wave: 20 coalesced loads per lane issued
 // back to back, then a cross-lane reduction.  Window <= 1280 samples.
 constexpr int ARGMAX_PER = 20;
-__device__ __forceinline__ bool am_beats(double v, int64_t vi, double b, int64_t bi) {
-  const bool vn = v != v, bn = b != b;
-  if (vn || bn) return vn && (!bn || vi < bi);
-  return v > b || (v == b && vi < bi);
-}
 __device__ inline void wave_argmax(const double* __restrict__ ds, int64_t i, int64_t wend, int lane, double& best,
                                    int64_t& bidx) {
   double vv[ARGMAX_PER];
@@ -70,6 +65,33 @@ __device__ inline void wave_argmax(const double* __restrict__ ds, int64_t i, int
     const int64_t oi = __shfl_xor(bidx, o);
     if (am_beats(ov, oi, best, bidx)) { best = ov; bidx = oi; }
   }
+}
+
+// wave_argmax from the sync tiles: whole tiles inside [i, wend) plus the raw
+// samples of the two ragged ends (one load per lane each instead of 20).
+__device__ inline void tile_argmax(const double* __restrict__ ds, const SyncTile* __restrict__ tiles, int64_t i,
+                                   int64_t wend, int lane, double& best, int64_t& bidx) {
+  const int64_t t0 = (i + 31) >> 5, t1 = wend >> 5;         // whole tiles [t0, t1)
+  if (t0 >= t1) { wave_argmax(ds, i, wend, lane, best, bidx); return; }
+  const int64_t h1 = t0 << 5, s1 = t1 << 5;               // raw [i, h1) and [s1, wend), < 32 each
+  double v = -__builtin_inf();
+  int64_t vi = 0x7fffffffffffffffLL;
+  {
+    const int64_t k = (lane < 32) ? i + lane : s1 + (lane - 32);
+    const bool in = (lane < 32) ? (k < h1) : (k < wend);
+    if (in) { v = ds[k]; vi = k; }
+  }
+  for (int64_t t = t0 + lane; t < t1; t += 64) {
+    const SyncTile T = tiles[t];
+    if (am_beats(T.v, T.idx, v, vi)) { v = T.v; vi = T.idx; }
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    const double ov = __shfl_xor(v, o);
+    const int64_t oi = __shfl_xor(vi, o);
+    if (am_beats(ov, oi, v, vi)) { v = ov; vi = oi; }
+  }
+  best = v;
+  bidx = vi;
 }
 
 // get_syncpeaks walk geometry for one read (lddecode_core.py:497-515).
@@ -110,7 +132,7 @@ extern "C" __global__ __launch_bounds__(64) void ldg_k_sync_walk(
     const int32_t* __restrict__ smap, const ReadDesc* __restrict__ reads, const double* __restrict__ video,
     int64_t vread_stride, int64_t vchan_stride, SysConst C, const int32_t* __restrict__ status,
     int32_t* __restrict__ node_pos, int32_t* __restrict__ node_pk, double* __restrict__ node_lv,
-    int32_t* __restrict__ node_n) {
+    int32_t* __restrict__ node_n, const SyncTile* __restrict__ stiles) {
   prio_latency();
 
   const int lane = threadIdx.x;
@@ -124,6 +146,7 @@ extern "C" __global__ __launch_bounds__(64) void ldg_k_sync_walk(
   const ReadDesc rd = reads[slot];
   const WalkGeom G(rd.n_out, C.linelen);
   const double* ds = video + (int64_t)slot * vread_stride + (int64_t)CH_SYNC * vchan_stride;
+  const SyncTile* tl = stiles + (int64_t)slot * STILE_PER_SLOT;
   int64_t i = (int64_t)k * G.seg;
   int64_t e = (k == SEG_K - 1) ? G.stop : (int64_t)(k + 1) * G.seg + G.ov;
   if (e > G.stop) e = G.stop;
@@ -134,7 +157,7 @@ extern "C" __global__ __launch_bounds__(64) void ldg_k_sync_walk(
   while (i < e && n < SEG_NMAX) {
     double best;
     int64_t bidx;
-    wave_argmax(ds, i, i + G.win, lane, best, bidx);
+    tile_argmax(ds, tl, i, i + G.win, lane, best, bidx);
     const bool pk = best > .2;
     if (lane == 0) { P[n] = (int32_t)i; K[n] = pk ? (int32_t)bidx : -1; V[n] = best; }
     n++;
@@ -150,7 +173,7 @@ extern "C" __global__ __launch_bounds__(64) void ldg_k_sync(
     const int32_t* __restrict__ smap, const ReadDesc* __restrict__ reads, const double* __restrict__ video, int64_t vread_stride,
     int64_t vchan_stride, SysConst C, FieldRec* __restrict__ recs, int32_t* __restrict__ peaks,
     const int32_t* __restrict__ status, const int32_t* __restrict__ node_pos, const int32_t* __restrict__ node_pk,
-    const double* __restrict__ node_lv, const int32_t* __restrict__ node_n) {
+    const double* __restrict__ node_lv, const int32_t* __restrict__ node_n, const SyncTile* __restrict__ stiles) {
   prio_latency();
 
   __shared__ int32_t s_npos[SEG_K * SEG_NMAX];
@@ -241,7 +264,7 @@ extern "C" __global__ __launch_bounds__(64) void ldg_k_sync(
         if (joined) break;
         double best;
         int64_t bidx;
-        wave_argmax(ds, p, p + G.win, lane, best, bidx);
+        tile_argmax(ds, stiles + (int64_t)slot * STILE_PER_SLOT, p, p + G.win, lane, best, bidx);
         if (best > .2) {
           if (np >= MAX_PEAKS) { overflow = true; break; }
           if (lane == 0) { s_pk[np] = (int32_t)bidx; s_lv[np] = best; }
