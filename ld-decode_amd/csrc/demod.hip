@@ -413,25 +413,34 @@ extern "C" __global__ __launch_bounds__(1024) void ldg_k_demod(
         if (in0 && in1) *reinterpret_cast<double2*>(o + p) = make_double2(z.x * inv, z.y * inv);
         else if (in0) o[p] = z.x * inv;
         else if (in1) o[p + 1] = z.y * inv;
-        if (kind == 4) {
-          // sync tile of outputs [p & ~31, +32): 16 lanes, np.argmax order
-          const int64_t n0 = (int64_t)off + p - BLOCKCUT;
-          double v = -__builtin_inf();
-          int64_t vi = 0x7fffffffffffffffLL;
-          if (in0) { v = z.x * inv; vi = n0; }
-          if (in1 && am_beats(z.y * inv, n0 + 1, v, vi)) { v = z.y * inv; vi = n0 + 1; }
+      }
+      if (kind == 4) {
+        // sync tiles (common.hpp SyncTile): tile j of this block = outputs
+        // [off + 32 j, +32) = block positions [1024 + 32 j, +32) = pairs
+        // m in [512 + 16 j, +16); threads 2j and 2j+1 scan one half each in
+        // order, then the halves combine (np.argmax order: the lower half wins ties)
+        const int j = t >> 1, hf = t & 1;
+        const int ntile = (copylen + 31) / 32;
+        double v = -__builtin_inf();
+        int64_t vi = 0x7fffffffffffffffLL;
+        const int64_t n0 = (int64_t)off + 32 * j;
+        if (j < ntile) {
 #pragma unroll
-          for (int o2 = 1; o2 < 16; o2 <<= 1) {
-            const double ov = __shfl_xor(v, o2);
-            const int64_t oi = __shfl_xor(vi, o2);
-            if (am_beats(ov, oi, v, vi)) { v = ov; vi = oi; }
+          for (int r = 0; r < 8; r++) {
+            const double2 z = X_[512 + 16 * j + 8 * hf + r];
+            const int e = 16 * hf + 2 * r;
+            if (e < copylen - 32 * j && am_beats(z.x * inv, n0 + e, v, vi)) { v = z.x * inv; vi = n0 + e; }
+            if (e + 1 < copylen - 32 * j && am_beats(z.y * inv, n0 + e + 1, v, vi)) { v = z.y * inv; vi = n0 + e + 1; }
           }
-          if ((t & 15) == 0 && p >= BLOCKCUT && p < BLOCKCUT + copylen) {
-            SyncTile tt;
-            tt.v = v;
-            tt.idx = vi;
-            stiles[(int64_t)slot * STILE_PER_SLOT + (n0 >> 5)] = tt;
-          }
+        }
+        const double ov = __shfl_xor(v, 1);
+        const int64_t oi = __shfl_xor(vi, 1);
+        if (am_beats(ov, oi, v, vi)) { v = ov; vi = oi; }
+        if (j < ntile && hf == 0) {
+          SyncTile tt;
+          tt.v = v;
+          tt.idx = vi;
+          stiles[(int64_t)slot * STILE_PER_SLOT + (n0 >> 5)] = tt;
         }
       }
       __syncthreads();
