@@ -60,14 +60,21 @@ def main(argv=None):
         return 1
 
     world = int(os.environ.get('WORLD_SIZE', '1'))
+    rccl = False
     if world > 1:
         # one process per GPU (python -m torch.distributed.run --nproc-per-node N lddecode.py ...):
-        # field-group sharding of the capture (ldgpu/shard.py); the exchange runs over gloo
+        # field-group sharding of the capture (ldgpu/shard.py).  The capture-window halo
+        # travels GPU to GPU over RCCL when every rank has its own GPU; the small summary
+        # exchange (all_gather_object) goes over gloo.
+        import torch
         import torch.distributed as dist
-        dist.init_process_group('gloo')
-        from ldgpu import native
-        ndev = max(1, native.load().ldg_device_count())
-        args.device = int(os.environ.get('LOCAL_RANK', '0')) % ndev
+        ndev = torch.cuda.device_count()
+        local = int(os.environ.get('LOCAL_RANK', '0'))
+        rccl = ndev >= world
+        if rccl:
+            torch.cuda.set_device(local)
+        dist.init_process_group('cpu:gloo,cuda:nccl' if rccl else 'gloo')
+        args.device = local % max(1, ndev)
         if args.comb:
             print("ERROR: --comb is single-GPU in this build")
             return 1
@@ -81,7 +88,10 @@ def main(argv=None):
 
     fmt = fmt_from_path(filename)
     raw = np.memmap(filename, dtype=np.uint8, mode='r')
-    dec.set_capture(raw, fmt)
+    if world == 1 or args.seek >= 0 or args.cut:
+        dec.set_capture(raw, fmt)
+    else:
+        dec.cap_bytes, dec.cap_nsamples, dec.fmt = infile_size, samples_in_bytes(fmt, infile_size), fmt
 
     if args.seek >= 0:
         nextsample = dec.findframe(args.seek, firstframe * samples_per_frame)
@@ -101,7 +111,7 @@ def main(argv=None):
 
     num_frames = req_frames if req_frames is not None else infile_size // bytes_per_frame - firstframe
     if world > 1:
-        return sharded(args, dec, outname, firstframe, num_frames, nextsample, req_frames)
+        return sharded(args, dec, outname, firstframe, num_frames, nextsample, req_frames, raw, fmt, rccl)
     tbc = open(outname + '.tbc', 'wb')
     pcm = open(outname + '.pcm', 'wb')
     rgb = open(outname + '.rgb', 'wb') if args.comb else None
@@ -128,7 +138,40 @@ def main(argv=None):
     return 0
 
 
-def sharded(args, dec, outname, firstframe, num_frames, nextsample, req_frames):
+def load_window(dec, raw, fmt, rank, world, start, rccl):
+    """This rank's capture window in HBM: its own samples read from storage, the tail
+    halo from the next rank (ldgpu/shard.py exchange_halo: RCCL between the capture
+    buffers, or gloo through host memory).  Returns what must stay alive."""
+    import torch
+    from ldgpu.shard import exchange_halo, sample_byte, shard_bounds, shard_windows, torch_p2p
+    nbytes = raw.size
+    bounds = shard_bounds(start, dec.cap_nsamples, dec.rf.samples_per_frame, world)
+    windows = shard_windows(bounds, dec.rf.samples_per_frame, dec.cap_nsamples)
+    lo, cut, hi = windows[rank]
+    end_b = lambda s: nbytes if s >= dec.cap_nsamples else sample_byte(fmt, s)   # noqa: E731
+    bl, bc, bh = sample_byte(fmt, lo), end_b(cut), end_b(hi)
+    if rccl:
+        buf = torch.empty(bh - bl, dtype=torch.uint8, device='cuda')
+        buf[:bc - bl].copy_(torch.from_numpy(np.ascontiguousarray(raw[bl:bc])))
+    else:
+        buf = torch.empty(bh - bl, dtype=torch.uint8)
+        buf[:bc - bl].numpy()[:] = raw[bl:bc]
+    got = exchange_halo(buf, rank, windows, fmt, torch_p2p)
+    if not got and bh > bc:                         # halo not held by the next rank: from storage
+        src = torch.from_numpy(np.ascontiguousarray(raw[bc:bh]))
+        buf[bc - bl:].copy_(src)
+    if rccl:
+        torch.cuda.synchronize()
+        dec.set_capture(None, fmt, device_ptr=buf.data_ptr(), nsamples=hi - lo, first_sample=lo,
+                        total_bytes=nbytes)
+    else:
+        dec.set_capture(buf.numpy(), fmt, first_sample=lo, total_bytes=nbytes)
+    print('rank %d: capture window samples [%d, %d), halo %s' % (rank, lo, hi,
+          'from rank %d over %s' % (rank + 1, 'RCCL' if rccl else 'gloo') if got else 'from storage'))
+    return buf
+
+
+def sharded(args, dec, outname, firstframe, num_frames, nextsample, req_frames, raw, fmt, rccl):
     """This rank's share of a field-group sharded decode; every rank writes its frames
     at their global offsets in the .tbc / .pcm, rank 0 writes the .json."""
     import torch.distributed as dist
@@ -140,8 +183,14 @@ def sharded(args, dec, outname, firstframe, num_frames, nextsample, req_frames):
         dist.all_gather_object(out, obj)
         return out
 
+    keep = load_window(dec, raw, fmt, rank, world, nextsample, rccl)    # noqa: F841 (buffer stays alive)
+
+    def whole():
+        print('rank %d: a read left the capture window; using the whole capture' % rank)
+        dec.set_capture(raw, fmt)
+
     res = decode_sharded(dec, rank, world, allgather, start_frame=firstframe, length=num_frames,
-                         start_sample=nextsample)
+                         start_sample=nextsample, whole_capture=whole)
     sizes = allgather((len(res), sum(a.nbytes for _, _, a, _ in res)))
     frame_bytes = dec.sysp.outlinelen * dec.sysp.frame_lines * 2
     first = sum(n for n, _ in sizes[:rank])

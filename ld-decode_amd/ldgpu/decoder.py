@@ -42,6 +42,10 @@ class ReferenceCrash(RuntimeError):
     """The reference decoder would have raised (uncaught) here."""
 
 
+class WindowMiss(RuntimeError):
+    """A read needs capture samples outside the resident window (sharded decode)."""
+
+
 def read_geometry(start):
     """Blocks of RFDecode.demod(start, 1e6) (lddecode_core.py:374-385): (s0, end, last block start)."""
     end = int(start + READLEN) + 1
@@ -139,6 +143,7 @@ class GPUDecoder:
         self.stats = {'batches': 0, 'reads': 0, 'reads_used': 0, 'gpu_s': 0.0, 'replay_s': 0.0}
         self.cap_bytes = None
         self.cap_nsamples = None
+        self.window = None          # (first, end) samples resident when a capture window is set
         self.cache = {}            # (start, mtf) -> (slot, info)
         self.hints = {}            # start -> absolute next start (start + nextfieldoffset)
         self._hint_keys = []       # sorted starts with hints
@@ -154,21 +159,34 @@ class GPUDecoder:
         self.archive, self.arch_next, self.shard_frames = False, 0, []
 
     # ---- capture ---------------------------------------------------------------
-    def set_capture(self, data, fmt, device_ptr=None, nsamples=None):
-        """Whole capture resident in HBM (data: bytes/ndarray, or a device pointer)."""
+    def set_capture(self, data, fmt, device_ptr=None, nsamples=None, first_sample=0, total_bytes=None):
+        """Capture resident in HBM (data: bytes/ndarray, or a device pointer).
+
+        A window of a larger capture (field-group sharding, ldgpu/shard.py): the
+        resident samples are [first_sample, first_sample + nsamples) of a capture
+        of total_bytes bytes; the frame accounting (EOF guard, frame count) uses the
+        whole capture, and a read that needs samples outside the window raises
+        WindowMiss instead of ending the decode."""
         if device_ptr is None:
             buf = np.frombuffer(data, dtype=np.uint8) if not isinstance(data, np.ndarray) else data.view(np.uint8)
             nbytes = buf.size
             nsamples = samples_in_bytes(fmt, nbytes)
-            self.ctx.set_capture(buf, nsamples, fmt, 0)
+            self.ctx.set_capture(buf, nsamples, fmt, first_sample)
         else:
             nbytes = bytes_for_samples(fmt, nsamples)
-            self.ctx.set_capture(None, nsamples, fmt, 0, device_ptr=device_ptr)
-        self.fmt, self.cap_bytes, self.cap_nsamples = fmt, nbytes, nsamples
+            self.ctx.set_capture(None, nsamples, fmt, first_sample, device_ptr=device_ptr)
+        if total_bytes is None:
+            self.window = None
+            self.fmt, self.cap_bytes, self.cap_nsamples = fmt, nbytes, nsamples
+        else:
+            self.window = (int(first_sample), int(first_sample) + int(nsamples))
+            self.fmt, self.cap_bytes = fmt, int(total_bytes)
+            self.cap_nsamples = samples_in_bytes(fmt, self.cap_bytes)
         self._reset_cache()
 
     def use_resident_capture(self, fmt, nsamples):
         """The capture already lives in this context's HBM (e.g. Context.synth)."""
+        self.window = None
         self.fmt, self.cap_nsamples = fmt, nsamples
         self.cap_bytes = bytes_for_samples(fmt, nsamples)
         self._reset_cache()
@@ -379,6 +397,11 @@ class GPUDecoder:
         slot, info = hit
         if info.status == native.FS_CRASH:
             raise ReferenceCrash('reference would raise at read %d' % readsample)
+        if info.status == native.FS_EOF and self.window is not None:
+            s0, _, last = read_geometry(key[0])
+            if s0 < self.window[0] or last + BLOCKLEN > self.window[1]:
+                if last + BLOCKLEN <= self.cap_nsamples:
+                    raise WindowMiss('read %d needs samples outside the window %s' % (key[0], self.window))
         f = GPUField(info, slot, int(readsample), mtf, audio_offset, self.sysp, None)
         f.tidx = len(self.transitions)       # audio-offset transitions before this field
         return f
@@ -556,10 +579,21 @@ class GPUDecoder:
         for k, v in (init_state or {}).items():        # chain state handed over by a previous shard
             setattr(self, k, v)
         nextsample = start_frame * spf if start_sample is None else start_sample
+        try:
+            return self._decode_loop(start_frame, num_frames, nextsample, spf, bpf, size, sink, stop_sample,
+                                     keep_from, firstframe)
+        finally:
+            while self.pending:                 # no launch outlives the call (an exception included)
+                self._launch_wait()
+            self.ctx.sync()
+
+    def _decode_loop(self, start_frame, num_frames, nextsample, spf, bpf, size, sink, stop_sample, keep_from,
+                     firstframe):
         done = 0
         nframes_read = 0
         hist = []
         W, H = self.sysp.outlinelen, self.sysp.frame_lines
+
         def more(ns):
             return stop_sample is None or ns < stop_sample
 
@@ -621,9 +655,6 @@ class GPUDecoder:
             if eof or (not frames and not launched and not self.pending):
                 break
             self._launch_wait()                 # the oldest launch: the replay continues into it
-        while self.pending:
-            self._launch_wait()
-        self.ctx.sync()
         return done
 
     def _flush(self, frames, W, H, sink):

@@ -26,8 +26,92 @@ Each rank decodes a contiguous range of the capture:
 The result is identical to a single decode of the whole capture:
 tests/test_shard.py checks it on the GPU, with ranks run one after another, and
 on CPU with gloo for the exchange logic.
+
+Capture windows (shard_windows / exchange_halo): a rank keeps only the samples
+its reads touch in HBM -- its own range from storage, [lo_k, cut_k), plus a
+tail halo [cut_k, hi_k) of the next shard's first samples (the last frames
+before B_{k+1} read up to two fields and one 1,000,001-sample read past it).
+The halo comes from rank k+1, which already holds those samples, over a
+point-to-point exchange: RCCL (torch.distributed 'nccl') between the GPUs'
+capture buffers when every rank has its own GPU, gloo through host memory
+otherwise.  A read that still falls outside the window raises WindowMiss and
+the rank re-runs with the whole capture.
 """
 import numpy as np
+
+from .decoder import WindowMiss
+from .formats import FMT_LDS, FMT_R30, FMT_S16, FMT_U8
+
+GROUP = 12                      # window cuts on whole packing groups of every format (3 and 4 samples)
+READ_SPAN = 1000001 + 2 * 16384  # a read's samples past its start (RFDecode.demod blocks)
+
+
+def sample_byte(fmt, s):
+    """Byte offset of sample s (s a multiple of GROUP)."""
+    return {FMT_U8: s, FMT_S16: 2 * s, FMT_R30: (s // 3) * 4, FMT_LDS: (s // 4) * 5}[fmt]
+
+
+def shard_windows(bounds, spf, nsamples, warmup_frames=2, halo_frames=2):
+    """Per rank (lo, cut, hi): the resident samples [lo, hi), read from storage
+    [lo, cut) and received from the next rank [cut, hi)."""
+    world = len(bounds) - 1
+    out = []
+    for k in range(world):
+        first = bounds[k] - (warmup_frames * spf if k else 0)
+        lo = max(0, (first - 1024) // GROUP * GROUP)
+        if k == world - 1:
+            cut = hi = nsamples
+        else:
+            cut = bounds[k + 1] // GROUP * GROUP
+            hi = min(nsamples, -(-(bounds[k + 1] + halo_frames * spf + READ_SPAN) // GROUP) * GROUP)
+        out.append((lo, cut, hi))
+    return out
+
+
+def halo_plan(windows):
+    """For each rank k < world-1: True if rank k+1 holds all of rank k's halo in the part
+    it reads from storage (then the halo travels rank k+1 -> k), else False (rank k
+    reads its halo from storage too).  The same on every rank."""
+    plan = []
+    for k in range(len(windows) - 1):
+        lo, cut, hi = windows[k]
+        nlo, ncut, _ = windows[k + 1]
+        plan.append(nlo <= cut and hi <= ncut)
+    return plan
+
+
+def exchange_halo(buf, rank, windows, fmt, p2p):
+    """Fill this rank's halo bytes of `buf` (the window's bytes, its own part already
+    in place) from the next rank, and send the previous rank its halo.  buf is
+    sliced by bytes; p2p([(kind, tensor, peer)]) runs the point-to-point transfers
+    (kind 'send' / 'recv') together, e.g. torch.distributed.batch_isend_irecv.
+    Returns True if this rank's halo came over the exchange."""
+    world = len(windows)
+    plan = halo_plan(windows)
+    lo, cut, hi = windows[rank]
+    ops = []
+    if rank > 0 and plan[rank - 1]:
+        plo, pcut, phi = windows[rank - 1]
+        a, b = sample_byte(fmt, pcut) - sample_byte(fmt, lo), sample_byte(fmt, phi) - sample_byte(fmt, lo)
+        ops.append(('send', buf[a:b], rank - 1))
+    got = False
+    if rank < world - 1 and plan[rank]:
+        a, b = sample_byte(fmt, cut) - sample_byte(fmt, lo), sample_byte(fmt, hi) - sample_byte(fmt, lo)
+        ops.append(('recv', buf[a:b], rank + 1))
+        got = True
+    if ops:
+        p2p(ops)
+    return got
+
+
+def torch_p2p(ops):
+    """exchange_halo's transfers over torch.distributed (RCCL for device tensors
+    under the 'nccl' backend, gloo for host tensors)."""
+    import torch.distributed as dist
+    reqs = dist.batch_isend_irecv([dist.P2POp(dist.isend if k == 'send' else dist.irecv, t, peer)
+                                   for k, t, peer in ops])
+    for r in reqs:
+        r.wait()
 
 
 def audio_next(offset, linecount, line_period):
@@ -86,8 +170,12 @@ def frame_offsets(summaries):
 class ShardedDecode:
     """One rank's part of a field-group sharded decode, in two phases."""
 
-    def __init__(self, dec, rank, world, start_frame=0, warmup_frames=2, length=None, start_sample=None):
+    def __init__(self, dec, rank, world, start_frame=0, warmup_frames=2, length=None, start_sample=None,
+                 whole_capture=None):
+        """whole_capture: callable that makes the whole capture resident (the fallback
+        when a capture window turns out too small)."""
         self.dec, self.rank, self.world = dec, rank, world
+        self.whole_capture, self.window_misses = whole_capture, 0
         self.spf = dec.rf.samples_per_frame
         # the whole decode's frame count limit (lddecode.py:49; -l): frames past it are dropped
         bpf = self.spf * 5 // 4
@@ -100,15 +188,24 @@ class ShardedDecode:
     def _run(self, sink, start_sample, keep_from, firstframe, init=None):
         dec = self.dec
         stop = self.bounds[self.rank + 1] if self.rank < self.world - 1 else None
-        self.frames = []
 
         def keep(pic, audio, meta):
             self.frames.append(pic)
             if sink:
                 sink(pic, None, meta)
 
-        dec.decode(start_sample=start_sample, stop_sample=stop, keep_from=keep_from, firstframe=firstframe,
-                   archive=True, sink=keep, init_state=init)
+        for attempt in range(2):
+            self.frames = []
+            try:
+                dec.decode(start_sample=start_sample, stop_sample=stop, keep_from=keep_from, firstframe=firstframe,
+                           archive=True, sink=keep, init_state=init)
+                return
+            except WindowMiss:
+                # a read outside this rank's capture window: decode from the whole capture
+                if attempt or self.whole_capture is None:
+                    raise
+                self.whole_capture()
+                self.window_misses += 1
 
     def local(self, sink=None):
         """Phase 1: decode this rank's range; returns the summary to exchange."""
@@ -167,11 +264,13 @@ class ShardedDecode:
         return out
 
 
-def decode_sharded(dec, rank, world, allgather, sink=None, start_frame=0, length=None, start_sample=None):
+def decode_sharded(dec, rank, world, allgather, sink=None, start_frame=0, length=None, start_sample=None,
+                   whole_capture=None):
     """Run all phases with `allgather(obj) -> [obj per rank]` (torch.distributed
     all_gather_object, or an in-process stand-in).  Returns this rank's
     [(global_index, frame, pcm, meta)]."""
-    sd = ShardedDecode(dec, rank, world, start_frame, length=length, start_sample=start_sample)
+    sd = ShardedDecode(dec, rank, world, start_frame, length=length, start_sample=start_sample,
+                       whole_capture=whole_capture)
     summ = allgather(sd.local())
     for _ in range(world):
         bad = check_chain(summ)

@@ -13,7 +13,9 @@ import pytest
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-from ldgpu.shard import audio_next, check_chain, frame_offsets, replay_offsets, shard_bounds, start_offsets
+from ldgpu.formats import FMT_LDS, FMT_R30, FMT_U8, bytes_for_samples
+from ldgpu.shard import (audio_next, check_chain, exchange_halo, frame_offsets, halo_plan, replay_offsets,
+                         sample_byte, shard_bounds, shard_windows, start_offsets)
 
 LINE_PERIOD = 63.5555555556
 
@@ -88,9 +90,63 @@ def test_exchange_over_gloo_world2():
     assert bad == [] and fo == [0, 4] and offs == start_offsets(s, LINE_PERIOD)
 
 
+SPF = 1334668
+
+
+def test_shard_windows_cover_every_shards_reads():
+    n = 60_000_000
+    b = shard_bounds(0, n, SPF, 4)
+    w = shard_windows(b, SPF, n)
+    assert halo_plan(w) == [True] * 3
+    for k, (lo, cut, hi) in enumerate(w):
+        assert lo % 12 == 0 and lo <= max(0, b[k] - 2 * SPF - 1024)
+        if k < 3:
+            assert cut <= b[k + 1] < cut + 12 and hi >= b[k + 1] + 2 * SPF + 1000001
+            assert w[k + 1][0] <= cut            # the next rank holds the halo in its own part
+        else:
+            assert cut == hi == n
+
+
+def _halo_worker(rank, world, port, fmt, q):
+    import torch
+    from ldgpu.shard import torch_p2p
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    n = 14_000_000
+    data = (np.arange(bytes_for_samples(fmt, n), dtype=np.uint64) * 2654435761 >> 13).astype(np.uint8)
+    w = shard_windows(shard_bounds(0, n, SPF, world), SPF, n)
+    lo, cut, hi = w[rank]
+    end = lambda s: data.size if s >= n else sample_byte(fmt, s)   # noqa: E731
+    bl, bc, bh = sample_byte(fmt, lo), end(cut), end(hi)
+    buf = torch.zeros(bh - bl, dtype=torch.uint8)
+    buf[:bc - bl].numpy()[:] = data[bl:bc]              # this rank's own part, from "storage"
+    got = exchange_halo(buf, rank, w, fmt, torch_p2p)
+    q.put((rank, got, bool(np.array_equal(buf.numpy(), data[bl:bh]))))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize('world,fmt', [(2, FMT_U8), (3, FMT_R30), (2, FMT_LDS)])
+def test_halo_exchange_over_gloo(world, fmt):
+    """Each rank's capture window = its own storage part + the halo from the next rank."""
+    with socket.socket() as sk:
+        sk.bind(('127.0.0.1', 0))
+        port = sk.getsockname()[1]
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_halo_worker, args=(r, world, port, fmt, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    out = dict((r, (g, ok)) for r, g, ok in (q.get(timeout=120) for _ in ps))
+    for p in ps:
+        p.join(timeout=60)
+    for r in range(world):
+        assert out[r][1], r
+        assert out[r][0] == (r < world - 1)
+
+
 @pytest.mark.gpu
-@pytest.mark.parametrize('world', [2, 3])
-def test_sharded_decode_equals_single_decode(world):
+@pytest.mark.parametrize('world,windowed', [(2, False), (3, False), (2, True), (3, True)])
+def test_sharded_decode_equals_single_decode(world, windowed):
     from ldgpu.decoder import GPUDecoder
     from ldgpu.shard import ShardedDecode
     from ldgpu.synth import make_capture
@@ -100,10 +156,18 @@ def test_sharded_decode_equals_single_decode(world):
     want = []
     ref.decode(sink=lambda fr, au, m: want.append((fr.copy(), au.copy(), m)))
     decs = [GPUDecoder(system='NTSC', batch=8) for _ in range(world)]
+    raw = np.frombuffer(data, np.uint8)
+    n = raw.size
+    w = shard_windows(shard_bounds(0, n, SPF - 1, world), SPF - 1, n)
     sds = []
     for r, d in enumerate(decs):
-        d.set_capture(data, 0)
-        sds.append(ShardedDecode(d, r, world))
+        if windowed:
+            # the window a rank holds after the halo exchange (the exchange itself: test_halo_exchange_over_gloo)
+            lo, cut, hi = w[r]
+            d.set_capture(raw[lo:hi], 0, first_sample=lo, total_bytes=n)
+        else:
+            d.set_capture(data, 0)
+        sds.append(ShardedDecode(d, r, world, whole_capture=lambda d=d: d.set_capture(data, 0)))
     summ = [sd.local() for sd in sds]
     assert check_chain(summ) == []
     got = []
@@ -114,3 +178,36 @@ def test_sharded_decode_equals_single_decode(world):
         assert gm == wm
         assert np.array_equal(gf, wf)
         assert np.array_equal(ga, wa)
+    if windowed:
+        assert all(sd.window_misses == 0 for sd in sds)
+
+
+@pytest.mark.gpu
+def test_sharded_window_miss_falls_back_to_whole_capture():
+    """A window too small for the reads (no halo) is detected (WindowMiss) and the rank
+    re-decodes from the whole capture: the result still equals the single decode."""
+    from ldgpu.decoder import GPUDecoder
+    from ldgpu.shard import ShardedDecode
+    from ldgpu.synth import make_capture
+    data = make_capture(int(40e6 * 0.6), 'u8', first_frame=1200, seed=21)
+    raw = np.frombuffer(data, np.uint8)
+    n = raw.size
+    ref = GPUDecoder(system='NTSC', batch=8)
+    ref.set_capture(data, 0)
+    want = []
+    ref.decode(sink=lambda fr, au, m: want.append((fr.copy(), au.copy(), m)))
+    w = shard_windows(shard_bounds(0, n, SPF - 1, 2), SPF - 1, n, halo_frames=0)
+    decs = [GPUDecoder(system='NTSC', batch=8) for _ in range(2)]
+    sds = []
+    for r, d in enumerate(decs):
+        lo, cut, _ = w[r]
+        d.set_capture(raw[lo:cut], 0, first_sample=lo, total_bytes=n)      # no halo at all
+        sds.append(ShardedDecode(d, r, 2, whole_capture=lambda d=d: d.set_capture(data, 0)))
+    summ = [sd.local() for sd in sds]
+    got = []
+    for sd in sds:
+        got += [(pic, a, m) for (g, a, m), pic in zip(sd.finish(summ), sd.frames)]
+    assert sds[0].window_misses == 1
+    assert len(got) == len(want)
+    for (gf, ga, gm), (wf, wa, wm) in zip(got, want):
+        assert gm == wm and np.array_equal(gf, wf) and np.array_equal(ga, wa)
