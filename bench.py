@@ -78,8 +78,13 @@ def main():
     if world > 1:
         import torch
         import torch.distributed as tdist
+        ndev = torch.cuda.device_count()
+        # one rank per GPU over RCCL; more ranks than GPUs (a rehearsal on a smaller
+        # box) share devices and exchange the timing scalars over gloo
+        use_nccl = ndev >= world
+        local = local % max(ndev, 1)
         torch.cuda.set_device(local)
-        tdist.init_process_group('nccl' if torch.cuda.is_available() else 'gloo')
+        tdist.init_process_group('nccl' if use_nccl else 'gloo')
         dist = tdist
 
     from ldgpu.decoder import GPUDecoder
@@ -124,7 +129,8 @@ def main():
 
     if dist is not None:
         import torch
-        t = torch.tensor([dt, float(frames), float(consumed)], dtype=torch.float64, device='cuda')
+        t = torch.tensor([dt, float(frames), float(consumed)], dtype=torch.float64,
+                         device='cuda' if tdist.get_backend() == 'nccl' else 'cpu')
         tmax = t.clone()
         dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
         dist.all_reduce(t, op=dist.ReduceOp.SUM)
