@@ -139,11 +139,12 @@ int ldg_set_capture(ldg_ctx* ctx, const void* data, int64_t nsamples, int fmt, i
  * host may cache reads across calls. */
 int ldg_decode_reads(ldg_ctx* ctx, int n, const int64_t* read_starts, const double* mtf, const int32_t* slots,
                      ldg_field_info* info);
-/* The same in two halves: launch without waiting (at most one outstanding per
- * context), then wait and fetch the records.  Output work (frames, audio,
- * archive, comb) runs on a second stream, so a host can replay and output one
- * batch while the next decodes.  The slots of an outstanding call are not
- * readable until its wait. */
+/* The same in two halves: launch without waiting, then wait and fetch the
+ * records of the OLDEST outstanding call.  Up to two calls may be outstanding:
+ * the second call's demod overlaps the first call's field kernels.  Slots of
+ * outstanding calls must be distinct and are not readable until their wait.
+ * Output work (frames, audio, archive, comb) runs on other streams, so a host
+ * can replay and output one batch while the next two decode. */
 int ldg_decode_reads_async(ldg_ctx* ctx, int n, const int64_t* read_starts, const double* mtf,
                            const int32_t* slots);
 int ldg_decode_reads_wait(ldg_ctx* ctx, ldg_field_info* info);
