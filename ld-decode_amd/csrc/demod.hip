@@ -346,11 +346,12 @@ extern "C" __global__ __launch_bounds__(1024) void ldg_k_demod(
       }
     }
     STAMP(5 + h);
-    fft8k_dit<true>(s_x, tw, tid);
+    double2 zr[8];
+    fft8k_dit<true, true>(s_x, tw, tid, zr);
     STAMP(6 + h);
 #pragma unroll
     for (int q = 0; q < 8; q++) {
-      const double2 z = X_[tid + T * q];
+      const double2 z = zr[q];
       const double a = atan2(z.y, z.x);
       if (h) tho[q] = a;
       else the[q] = a;
@@ -397,7 +398,8 @@ extern "C" __global__ __launch_bounds__(1024) void ldg_k_demod(
     const double2* G = kind == 0 ? g_video : kind == 1 ? g_burst : kind == 2 ? g_pilot : kind == 3 ? g_05 : g_psync;
     merge_pairs(X_, twk, G, tid, D);
     STAMP(12 + 3 * e);
-    fft8k_dit<true>(s_x, tw, tid);
+    double2 zr[8];                               // outputs at natural positions t + T q
+    fft8k_dit<true, true>(s_x, tw, tid, zr);
     STAMP(13 + 3 * e);
     const int t = fresh(tid);
     if (kind != 3) {
@@ -407,7 +409,7 @@ extern "C" __global__ __launch_bounds__(1024) void ldg_k_demod(
       for (int q = 0; q < 8; q++) {
         const int m = t + T * q;
         const int p = 2 * m;
-        const double2 z = X_[m];
+        const double2 z = zr[q];
         const bool in0 = p >= BLOCKCUT && p < BLOCKCUT + copylen;
         const bool in1 = p + 1 >= BLOCKCUT && p + 1 < BLOCKCUT + copylen;
         if (in0 && in1) *reinterpret_cast<double2*>(o + p) = make_double2(z.x * inv, z.y * inv);
@@ -415,6 +417,9 @@ extern "C" __global__ __launch_bounds__(1024) void ldg_k_demod(
         else if (in1) o[p + 1] = z.y * inv;
       }
       if (kind == 4) {
+#pragma unroll
+        for (int q = 0; q < 8; q++) X_[t + T * q] = zr[q];
+        __syncthreads();
         // sync tiles (common.hpp SyncTile): tile j of this block = outputs
         // [off + 32 j, +32) = block positions [1024 + 32 j, +32) = pairs
         // m in [512 + 16 j, +16); threads 2j and 2j+1 scan one half each in
@@ -447,8 +452,7 @@ extern "C" __global__ __launch_bounds__(1024) void ldg_k_demod(
     } else {
       double v0[8], v1[8];
 #pragma unroll
-      for (int q = 0; q < 8; q++) { const double2 z = X_[t + T * q]; v0[q] = z.x * inv; v1[q] = z.y * inv; }
-      __syncthreads();
+      for (int q = 0; q < 8; q++) { const double2 z = zr[q]; v0[q] = z.x * inv; v1[q] = z.y * inv; }
       double* o = vout + (int64_t)CH_05 * vchan_stride;
 #pragma unroll
       for (int q = 0; q < 8; q++) {

@@ -140,8 +140,14 @@ __device__ __forceinline__ void fft8k_dif(double2* __restrict__ s, const double2
 }
 
 // Transform of a digit-reversed input (the transpose of fft8k_dif), natural order out.
-template <bool INV>
-__device__ __forceinline__ void fft8k_dit(double2* __restrict__ s, const double2* __restrict__ tw, int tid) {
+// OUT_REGS: the last stage leaves its outputs in registers instead of LDS --
+// thread tid holds natural positions tid + 1024 q in out[q], q < 8 (the layout a
+// caller reading X_[tid + 1024 q] would get) -- saving an LDS round trip for an
+// elementwise consumer.  The transform then ends with the barrier after its last
+// LDS reads, so the caller may write s right away.
+template <bool INV, bool OUT_REGS = false>
+__device__ __forceinline__ void fft8k_dit(double2* __restrict__ s, const double2* __restrict__ tw, int tid,
+                                          double2* out = nullptr) {
   __syncthreads();
   {
     asm volatile("" : "+v"(tid));
@@ -198,8 +204,14 @@ __device__ __forceinline__ void fft8k_dit(double2* __restrict__ s, const double2
     }
     dft8<INV>(u);
     __syncthreads();
+    if constexpr (OUT_REGS) {
 #pragma unroll
-    for (int r1 = 0; r1 < 8; r1++) s[sm + 512 * (2 * r1 + b)] = u[r1];
+      for (int r1 = 0; r1 < 8; r1++) out[r1] = u[r1];
+      return;
+    } else {
+#pragma unroll
+      for (int r1 = 0; r1 < 8; r1++) s[sm + 512 * (2 * r1 + b)] = u[r1];
+    }
   }
   __syncthreads();
 }
