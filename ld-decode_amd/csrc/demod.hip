@@ -196,10 +196,9 @@ extern "C" __global__ __launch_bounds__(1024) void ldg_k_demod(
     const double2* __restrict__ a_lfilt, const double2* __restrict__ a_rfilt, SysConst C,
     double* __restrict__ video, int64_t vread_stride, int64_t vchan_stride,
     double* __restrict__ audio1, int64_t aread_stride, int64_t achan_stride, int32_t* __restrict__ status,
-    double2* __restrict__ ospill, SyncTile* __restrict__ stiles) {
+    double2* __restrict__ ospill, SyncTile* __restrict__ stiles, double2* __restrict__ aslice) {
   __shared__ double2 s_x[M];          // 128 KiB: the 8192-point transforms
-  __shared__ double2 s_a[2048];       // 32 KiB: the two 1024-point audio transforms
-  const CBuf X_{s_x}, A_{s_a};
+  const CBuf X_{s_x};
   const int tid = threadIdx.x;
   STAMP(0);
   const int slot = smap[blockIdx.x / MAX_BLOCKS_PER_READ];
@@ -273,8 +272,10 @@ extern "C" __global__ __launch_bounds__(1024) void ldg_k_demod(
       double2 xk = rsplit(X_[dr_pos(k)], X_[dr_pos(M - k)], tw[k]);
       if (mir) xk = conj2(xk);
       const double2 al = cmul(xk, a_lfilt[j]), ar = cmul(xk, a_rfilt[j]);
-      A_[j] = al;                       // left at [0,1024), right at [1024,2048)
-      A_[1024 + j] = ar;
+      // per slot (a later call's demod must not overwrite slices ldg_k_audio1 has not read)
+      double2* as = aslice + ((int64_t)slot * MAX_BLOCKS_PER_READ + b) * 2048;   // left [0,1024), right [1024,2048)
+      as[j] = al;
+      as[1024 + j] = ar;
     }
     __syncthreads();
     const int t = fresh(tid);
@@ -297,37 +298,9 @@ extern "C" __global__ __launch_bounds__(1024) void ldg_k_demod(
   }
 
   STAMP(3);
-  // ---- 3. audio phase 1: 2 x IFFT1024 -> FM demod (lddecode_core.py:321-328) ----
-  {
-    const int g = tid >> 9, lt = tid & 511;
-    const CBuf ga = A_ + (g ? 1024 : 0);
-    fft_lds<1024, 512, true>(ga, tw, lt);
-    double th[2];
-#pragma unroll
-    for (int e = 0; e < 2; e++) { const double2 z = ga[lt + 512 * e]; th[e] = atan2(z.y, z.x); }
-    __syncthreads();
-    double* gth = reinterpret_cast<double*>(s_a) + (g ? 1024 : 0);     // plain (unswizzled) phase scratch
-#pragma unroll
-    for (int e = 0; e < 2; e++) gth[lt + 512 * e] = th[e];
-    __syncthreads();
-    double* aout = audio1 + (int64_t)slot * aread_stride + (int64_t)g * achan_stride;
-    const int kept = copylen / AUDIO_DIV1;
-#pragma unroll
-    for (int e = 0; e < 2; e++) {
-      const int p = lt + 512 * e;
-      const double prev = p ? gth[p - 1] : 0.0;
-      const double d = p ? fold_tau(th[e] - prev) : 0.0;
-      const double v = d * (C.freq_arf / TAU) + C.audio_lowfreq;
-      const int j = p - BLOCKCUT / AUDIO_DIV1;
-      if (j >= 0 && j < kept) aout[off / AUDIO_DIV1 + j] = v;
-    }
-    // zero the tail the reference leaves at 0 (np.zeros) after the last block
-    if (b == rd.n_blocks - 1) {
-      const int last = (off + copylen) / AUDIO_DIV1;
-      for (int j = last + lt; j < rd.n_audio; j += 512) aout[j] = 0.0;
-    }
-  }
-
+  // (audio phase 1 -- 2 x IFFT1024 -> FM demod -- runs in ldg_k_audio1 on the
+  // slices above: the demod keeps 128 KiB of LDS, so kernels with up to 32 KiB
+  // share its CUs)
   STAMP(4);
   // ---- 4. analytic IFFTs (even, odd) -> instantaneous phase --------------------
   // One loop body for both halves: one copy of the inverse FFT in the code (the
@@ -475,6 +448,61 @@ extern "C" __global__ __launch_bounds__(1024) void ldg_k_demod(
     }
     STAMP(14 + 3 * e);
   }
+}
+
+// ---------------------------------------------------------------------------
+// Audio phase 1 (lddecode_core.py:321-328): per overlap-save block, the two
+// carrier slices the demod filtered (aslice, 2 x 1024 bins) -> 1024-point IFFT
+// -> unwrap_hilbert at 2.5 MHz + the low carrier -> the block's kept audio
+// samples.  grid: n_reads * MAX_BLOCKS_PER_READ workgroups of 1024 threads
+// (threads [0,512) left, [512,1024) right).
+extern "C" __global__ __launch_bounds__(1024) void ldg_k_audio1(
+    const int32_t* __restrict__ smap, const ReadDesc* __restrict__ reads, const double2* __restrict__ tw, SysConst C,
+    const double2* __restrict__ aslice, double* __restrict__ audio1, int64_t aread_stride, int64_t achan_stride,
+    const int32_t* __restrict__ status) {
+  __shared__ double2 s_a[2048];
+  const CBuf A_{s_a};
+  const int tid = threadIdx.x;
+  const int slot = smap[blockIdx.x / MAX_BLOCKS_PER_READ];
+  const int b = blockIdx.x % MAX_BLOCKS_PER_READ;
+  const ReadDesc rd = reads[slot];
+  if (b >= rd.n_blocks || status[slot] == FS_EOF) return;
+  const int off = b * BLOCKSTEP;
+  const int copylen = (off + (BLOCKLEN - BLOCKCUT) > rd.n_out) ? rd.n_out - off : BLOCKSTEP;
+  constexpr double TAU = 6.283185307179586;
+  const double2* as = aslice + ((int64_t)slot * MAX_BLOCKS_PER_READ + b) * 2048;
+  A_[tid] = as[tid];
+  A_[1024 + tid] = as[1024 + tid];
+  {
+    const int g = tid >> 9, lt = tid & 511;
+    const CBuf ga = A_ + (g ? 1024 : 0);
+    fft_lds<1024, 512, true>(ga, tw, lt);
+    double th[2];
+#pragma unroll
+    for (int e = 0; e < 2; e++) { const double2 z = ga[lt + 512 * e]; th[e] = atan2(z.y, z.x); }
+    __syncthreads();
+    double* gth = reinterpret_cast<double*>(s_a) + (g ? 1024 : 0);     // plain (unswizzled) phase scratch
+#pragma unroll
+    for (int e = 0; e < 2; e++) gth[lt + 512 * e] = th[e];
+    __syncthreads();
+    double* aout = audio1 + (int64_t)slot * aread_stride + (int64_t)g * achan_stride;
+    const int kept = copylen / AUDIO_DIV1;
+#pragma unroll
+    for (int e = 0; e < 2; e++) {
+      const int p = lt + 512 * e;
+      const double prev = p ? gth[p - 1] : 0.0;
+      const double d = p ? fold_tau(th[e] - prev) : 0.0;
+      const double v = d * (C.freq_arf / TAU) + C.audio_lowfreq;
+      const int j = p - BLOCKCUT / AUDIO_DIV1;
+      if (j >= 0 && j < kept) aout[off / AUDIO_DIV1 + j] = v;
+    }
+    // zero the tail the reference leaves at 0 (np.zeros) after the last block
+    if (b == rd.n_blocks - 1) {
+      const int last = (off + copylen) / AUDIO_DIV1;
+      for (int j = last + lt; j < rd.n_audio; j += 512) aout[j] = 0.0;
+    }
+  }
+
 }
 
 // ---------------------------------------------------------------------------
