@@ -48,6 +48,8 @@ def parse():
     ap.add_argument('--cpu-seconds', type=float, default=1.0, help='oracle baseline sample (seconds of RF)')
     ap.add_argument('--no-cpu', action='store_true')
     ap.add_argument('--no-comb', action='store_true', help='stop at .tbc (skip the 2D comb stage)')
+    ap.add_argument('--prof-all', action='store_true',
+                    help='HIP-event timing of every kernel (default: the demod only, the roofline kernel)')
     return ap.parse_args()
 
 
@@ -109,7 +111,7 @@ def main():
             torch.cuda.synchronize()
             dist.barrier()
 
-    dec.ctx.profile(True)
+    dec.ctx.profile(True if args.prof_all else 'demod')
     reads0 = dec.stats['reads']
     barrier()
     t0 = time.perf_counter()

@@ -201,7 +201,9 @@ typedef struct ldg_kernel_stat {
   int64_t launches;
   double total_ms; /* sum of per-launch event durations */
 } ldg_kernel_stat;
-/* on != 0: record a start/stop event pair around every kernel launch (resets stats). */
+/* on == 1: record a start/stop event pair around every kernel launch; on == 2:
+ * around the demod only (the roofline kernel; two events per call instead of
+ * ~30); 0: off.  Resets the stats. */
 int ldg_profile_enable(ldg_ctx* ctx, int on);
 /* Copy up to max per-kernel records; returns the number of kernels recorded. */
 int ldg_profile_read(ldg_ctx* ctx, ldg_kernel_stat* out, int max);

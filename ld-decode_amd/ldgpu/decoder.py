@@ -17,6 +17,7 @@ Audio offsets (:1289, :484) are a scalar recurrence computed here with the
 reference's own numpy arithmetic; the per-sample audio resampling runs on the
 GPU for all fields of a batch at once.
 """
+import math
 import os
 import time
 
@@ -67,12 +68,29 @@ def loader_tell(fmt, sample, nbytes):
     return start + max(0, min(need, nbytes - start))
 
 
+def arange_last(start, stop, step):
+    """np.arange(start, stop, step, dtype=float64)[-1] without the array: numpy's
+    length ceil((stop - start) / step) and its fill rule (element i = start +
+    i * ((start + step) - start) from the third on; numpy/_core/src/multiarray/
+    ctors.c PyArray_ArangeObj and the DOUBLE fill)."""
+    n = math.ceil((stop - start) / step)
+    if n < 1:
+        raise ValueError('empty arange')
+    if n == 1:
+        return start
+    nxt = start + step
+    if n == 2:
+        return nxt
+    return start + float(n - 1) * (nxt - start)
+
+
 class GPUField:
-    """Field-like view of one decoded read (attributes of lddecode_core.Field)."""
+    """Field-like view of one decoded read (attributes of lddecode_core.Field).
+    The VBI / line-code dicts are built on first use."""
 
     __slots__ = ('info', 'slot', 'readsample', 'mtf_level', 'audio_offset', 'valid', 'istop', 'linecount',
-                 'nextfieldoffset', 'npeaks', 'nvsync', 'vbi', 'linecode', 'tbcstart', 'status',
-                 'audio_next_offset', 'nextsample', 'dsaudio_used', 'tidx')
+                 'nextfieldoffset', 'npeaks', 'nvsync', '_vbi', '_linecode', 'tbcstart', 'status',
+                 'audio_next_offset', 'nextsample', 'dsaudio_used', 'tidx', 'sysp')
 
     def __init__(self, info, slot, readsample, mtf, audio_offset, sysp, frametime_lines):
         self.info, self.slot, self.readsample, self.mtf_level = info, slot, readsample, mtf
@@ -85,23 +103,35 @@ class GPUField:
         self.npeaks, self.nvsync = info.npeaks, info.nvsync
         self.tbcstart = info.tbcstart
         self.dsaudio_used = False
+        self.sysp = sysp
+        self._vbi = self._linecode = None
         if self.valid:
-            def v(x):
-                return None if x == native.VBI_NONE else int(x)
-            self.vbi = {'minutes': v(info.vbi_minutes), 'seconds': v(info.vbi_seconds),
-                        'clvframe': v(info.vbi_clvframe), 'framenr': v(info.vbi_framenr),
-                        'statuscode': None, 'status': v(info.vbi_status), 'isclv': bool(info.vbi_isclv)}
-            self.linecode = {str(sysp.codelines[q]): ([int(x) for x in info.linecode[q]] if info.linecode_ok[q] else None)
-                             for q in range(3)}
             # downscale_audio's returned next offset (lddecode_core.py:432-437,484)
             frametime = (sysp.line_period * self.linecount) / 1000000
             gap = 1 / 48000.0
-            ticks = np.arange(audio_offset, frametime + gap, gap, dtype=np.double)
-            self.audio_next_offset = ticks[-1] - frametime
+            self.audio_next_offset = arange_last(audio_offset, frametime + gap, gap) - frametime
         else:
-            self.vbi = None
-            self.linecode = None
             self.audio_next_offset = audio_offset
+
+    @property
+    def vbi(self):
+        if self._vbi is None and self.valid:
+            info = self.info
+
+            def v(x):
+                return None if x == native.VBI_NONE else int(x)
+            self._vbi = {'minutes': v(info.vbi_minutes), 'seconds': v(info.vbi_seconds),
+                         'clvframe': v(info.vbi_clvframe), 'framenr': v(info.vbi_framenr),
+                         'statuscode': None, 'status': v(info.vbi_status), 'isclv': bool(info.vbi_isclv)}
+        return self._vbi
+
+    @property
+    def linecode(self):
+        if self._linecode is None and self.valid:
+            info = self.info
+            self._linecode = {str(self.sysp.codelines[q]): (list(info.linecode[q]) if info.linecode_ok[q] else None)
+                              for q in range(3)}
+        return self._linecode
 
     def record(self):
         rec = {'readsample': int(self.readsample), 'nextsample': int(self.nextsample), 'valid': bool(self.valid),

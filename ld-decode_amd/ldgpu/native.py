@@ -295,7 +295,9 @@ class Context:
 
     # ---- profiling / tooling -------------------------------------------------------
     def profile(self, on=True):
-        self._check(self.lib.ldg_profile_enable(self.h, 1 if on else 0), 'ldg_profile_enable')
+        """on: True (every kernel), 'demod' (the demod only), False."""
+        mode = 2 if on == 'demod' else (1 if on else 0)
+        self._check(self.lib.ldg_profile_enable(self.h, mode), 'ldg_profile_enable')
 
     def profile_stats(self):
         arr = (KernelStat * 64)()

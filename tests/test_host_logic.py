@@ -86,3 +86,21 @@ def test_predictor_is_exact_for_stable_ntsc():
     """r[k] = r[k-6] + 4,004,000 (3 NTSC frames at 40 MSPS is an integer number of samples)."""
     t = RFTables('NTSC')
     assert t.freq_hz * 3 / t.system.fps == pytest.approx(4004000, abs=1e-6)
+
+
+def test_arange_last_matches_numpy():
+    """GPUField's audio offset recurrence uses np.arange(...)[-1] without the array
+    (downscale_audio, lddecode_core.py:432-437, 484): bit-identical to numpy."""
+    from ldgpu.decoder import arange_last
+    rng = np.random.default_rng(7)
+    gap = 1 / 48000.0
+    for i in range(20000):
+        start = float(rng.uniform(0, gap))
+        lc = int(rng.integers(250, 320))
+        ft = (63.5555555556 * lc) / 1000000
+        assert arange_last(start, ft + gap, gap) == np.arange(start, ft + gap, gap, dtype=np.double)[-1]
+    for i in range(5000):
+        st = float(rng.uniform(-5, 5))
+        step = float(rng.uniform(1e-4, 1))
+        stop = st + float(rng.uniform(step, 100 * step))
+        assert arange_last(st, stop, step) == np.arange(st, stop, step)[-1]
