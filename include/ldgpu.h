@@ -155,6 +155,12 @@ int ldg_decode_reads_wait(ldg_ctx* ctx, ldg_field_info* info);
 int ldg_field_audio(ldg_ctx* ctx, int n, const int32_t* slots, const double* offsets, int16_t* pcm,
                     int64_t pcm_stride, int32_t* counts, double* next_offsets);
 
+/* ldg_field_audio in two halves (one outstanding): launch, so the kernel and
+ * the copies overlap the host's next batch, then collect into the caller's
+ * arrays (as ldg_field_audio would have filled them). */
+int ldg_field_audio_async(ldg_ctx* ctx, int n, const int32_t* slots, const double* offsets);
+int ldg_field_audio_collect(ldg_ctx* ctx, int16_t* pcm, int64_t pcm_stride, int32_t* counts, double* next_offsets);
+
 /* Field archive (field-group sharding): keep the inputs of
  * ldg_field_audio of n live slots (field record, final line locations, 625 kHz
  * audio) at archive entries first..first+n-1, so a field's 48 kHz audio can be

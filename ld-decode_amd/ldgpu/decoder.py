@@ -187,6 +187,7 @@ class GPUDecoder:
         self.depth = int(os.environ.get('LDG_DEPTH', '2'))   # launches kept in flight in steady state
         self.transitions = []              # audio-offset chain: linecount of each transition's field
         self.archive, self.arch_next, self.shard_frames = False, 0, []
+        self._out_pending = None           # (frames, pics, audio fields, sink) awaiting their audio
 
     # ---- capture ---------------------------------------------------------------
     def set_capture(self, data, fmt, device_ptr=None, nsamples=None, first_sample=0, total_bytes=None):
@@ -615,7 +616,11 @@ class GPUDecoder:
         finally:
             while self.pending:                 # no launch outlives the call (an exception included)
                 self._launch_wait()
-            self.ctx.sync()
+            try:
+                self._emit_pending()
+            finally:
+                self._out_pending = None
+                self.ctx.sync()
 
     def _decode_loop(self, start_frame, num_frames, nextsample, spf, bpf, size, sink, stop_sample, keep_from,
                      firstframe):
@@ -718,8 +723,19 @@ class GPUDecoder:
                                           'mtf': float(fr.top.mtf_level)})
             self.arch_next += len(af)
             af = []
-        if af:
-            pcm, counts, _ = self.ctx.field_audio([x.slot for _, x in af], [x.audio_offset for _, x in af])
+        # the audio runs while the host plans and replays the next batch: this batch's
+        # frames go to the sink at the next flush (or at the end of the decode)
+        self._emit_pending()
+        self.ctx.field_audio_async([x.slot for _, x in af], [x.audio_offset for _, x in af])
+        self._out_pending = (frames, pics, af, sink)
+
+    def _emit_pending(self):
+        """Collect the outstanding batch's audio and hand its frames to the sink."""
+        if self._out_pending is None:
+            return
+        frames, pics, af, sink = self._out_pending
+        self._out_pending = None
+        pcm, counts, _ = self.ctx.field_audio_collect()
         per_frame = [[] for _ in frames]
         for j, (fr_i, x) in enumerate(af):
             if counts[j] < 0:

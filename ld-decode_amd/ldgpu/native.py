@@ -21,7 +21,8 @@ EXPORTS = ['ldg_create', 'ldg_destroy', 'ldg_last_error', 'ldg_set_filters', 'ld
            'ldg_decode_reads', 'ldg_field_audio', 'ldg_assemble_frames', 'ldg_debug_read',
            'ldg_comb_ntsc', 'ldg_comb_reset', 'ldg_version', 'ldg_device_count', 'ldg_profile_enable',
            'ldg_profile_read', 'ldg_synth_capture', 'ldg_capture_download', 'ldg_comb_ntsc_async', 'ldg_sync',
-           'ldg_archive_fields', 'ldg_archive_audio', 'ldg_decode_reads_async', 'ldg_decode_reads_wait']
+           'ldg_archive_fields', 'ldg_archive_audio', 'ldg_decode_reads_async', 'ldg_decode_reads_wait',
+           'ldg_field_audio_async', 'ldg_field_audio_collect']
 
 
 class FieldInfo(C.Structure):
@@ -90,6 +91,8 @@ def load(path=None):
                                      C.POINTER(C.c_int32), C.POINTER(FieldInfo)]
     lib.ldg_field_audio.argtypes = [vp, C.c_int, C.POINTER(C.c_int32), C.POINTER(C.c_double),
                                     C.POINTER(C.c_int16), C.c_int64, C.POINTER(C.c_int32), C.POINTER(C.c_double)]
+    lib.ldg_field_audio_async.argtypes = [vp, C.c_int, vp, vp]
+    lib.ldg_field_audio_collect.argtypes = [vp, vp, C.c_int64, vp, vp]
     lib.ldg_assemble_frames.argtypes = [vp, C.c_int, C.POINTER(C.c_int32), C.POINTER(C.c_int32),
                                         C.POINTER(C.c_uint16), C.c_int]
     lib.ldg_debug_read.argtypes = [vp, C.c_int, C.c_int, vp, C.c_int64]
@@ -226,6 +229,24 @@ class Context:
         of = np.ascontiguousarray(offsets, dtype=np.float64)
         self._check(self.lib.ldg_field_audio(self.h, n, _ptr(sl, C.c_int32), _ptr(of), _ptr(pcm, C.c_int16), stride,
                                              _ptr(counts, C.c_int32), _ptr(nxt)), 'ldg_field_audio')
+        return pcm[:n], counts[:n], nxt[:n]
+
+    def field_audio_async(self, slots, offsets):
+        """Launch ldg_field_audio_async; field_audio_collect() returns what field_audio would."""
+        sl = np.ascontiguousarray(slots, dtype=np.int32)
+        of = np.ascontiguousarray(offsets, dtype=np.float64)
+        self._check(self.lib.ldg_field_audio_async(self.h, sl.size, sl.ctypes.data, of.ctypes.data),
+                    'ldg_field_audio_async')
+        self._audio_n = sl.size
+
+    def field_audio_collect(self):
+        n = self._audio_n
+        stride = 2048
+        pcm = np.zeros((max(n, 1), stride), dtype=np.int16)
+        counts = np.zeros(max(n, 1), dtype=np.int32)
+        nxt = np.zeros(max(n, 1), dtype=np.float64)
+        self._check(self.lib.ldg_field_audio_collect(self.h, pcm.ctypes.data, stride, counts.ctypes.data,
+                                                     nxt.ctypes.data), 'ldg_field_audio_collect')
         return pcm[:n], counts[:n], nxt[:n]
 
     def archive_fields(self, slots, first):
