@@ -451,93 +451,179 @@ extern "C" __global__ __launch_bounds__(64) void ldg_k_burst_field(const int32_t
 }
 
 // Final resample of 'demod' (lineoffset 1 NTSC / 3 PAL, wow) to uint16 .tbc
-// lines (lddecode_core.py:1135-1159 NTSC, :1023-1035 PAL).
-// grid: n_reads * FINAL_GROUPS workgroups of FINAL_NT threads; a workgroup
-// resamples FINAL_LPW consecutive lines, loading the next line's samples into
-// registers while it solves the current one (the loads are off the critical path).
+// lines (lddecode_core.py:1135-1159 NTSC, :1023-1035 PAL): the whole-line
+// not-a-knot spline of spline_block, with the samples read from the demod
+// channel in HBM / L2 (each thread its own rows into registers, the
+// evaluation's two knots per output straight from the channel) and only the
+// second derivatives in LDS.  ~25 KiB of LDS per workgroup, so a final-pass
+// workgroup fits beside a demod workgroup (128 KiB) on one CU.
+// grid: n_reads * MAX_LINES workgroups of FINAL_NT threads, one line each.
 constexpr int FINAL_NT = 256;
-constexpr int FINAL_LPW = 4;
-constexpr int FINAL_GROUPS = MAX_LINES / FINAL_LPW;
-constexpr int FINAL_PF = (SPL_MAXN + FINAL_NT - 1) / FINAL_NT;     // samples per thread per line
+constexpr int FINAL_CHMAX = ((SPL_MAXN + FINAL_NT - 1) / FINAL_NT) | 1;   // rows per thread, upper bound
+struct FinalLDS {
+  double ms[SPL_MAXN + 1];
+  double ct[17];
+  double wa[FINAL_NT / 64], wb[FINAL_NT / 64];
+  double carry[FINAL_NT];
+  double m1, mn1;
+};
 extern "C" __global__ __launch_bounds__(FINAL_NT) void ldg_k_final_lines(
     const int32_t* __restrict__ smap, const double* __restrict__ video, int64_t vread_stride, int64_t vchan_stride,
     SysConst C, FieldRec* __restrict__ recs, const double* __restrict__ lines, const float* __restrict__ blevel,
     uint16_t* __restrict__ pic, int64_t pic_stride) {
   prio_latency();
-  __shared__ SplineLDS<FINAL_NT> S;
+  __shared__ FinalLDS S;
   const int tid = threadIdx.x;
-  const int slot = smap[blockIdx.x / FINAL_GROUPS];
-  const int row0 = (blockIdx.x % FINAL_GROUPS) * FINAL_LPW;
+  const int slot = smap[blockIdx.x / MAX_LINES];
+  const int row = blockIdx.x % MAX_LINES;
   FieldRec* R = recs + slot;
   if (R->status != FS_PENDING) return;
   const int lc = R->linecount;
-  if (row0 >= lc) return;
-  const int row1 = (row0 + FINAL_LPW < lc) ? row0 + FINAL_LPW : lc;
+  if (row >= lc) return;
   const int loff = (C.system == 1) ? 3 : 1;
+  const int l = row + loff;
   const double* lf = lines + (int64_t)slot * LINES_STRIDE + LLF * MAX_LINES;
   const double* dm = video + (int64_t)slot * vread_stride + (int64_t)CH_DEMOD * vchan_stride;
   const int64_t len = R->n_out;
   const int W = C.outlinelen;
+  uint16_t* out = pic + (int64_t)slot * pic_stride + (int64_t)row * W;
+  const double begin = lf[l], end = lf[l + 1];
+  // ---- geometry (spline_block): y[j] = dm[ib + j], j = 0..n
+  const int64_t ib = py_int(begin), ie = py_int(end);
+  const int64_t n64 = ie - ib;
+  if (ib < 0 || n64 < 6 || n64 >= SPL_MAXN || ib + n64 + 1 > len) {
+    if (tid == 0) R->status = FS_TBC;
+    return;
+  }
+  const int n = (int)n64;
+  const double* y = dm + ib;
+  if (tid < 17) S.ct[tid] = g_ctab.v[tid];
+  if (tid == 0) {
+    S.m1 = (6.0 * ((y[2] - y[1]) - (y[1] - y[0]))) / 6.0;
+    S.mn1 = (6.0 * ((y[n] - y[n - 1]) - (y[n - 1] - y[n - 2]))) / 6.0;
+  }
+  // rows j = lo + t, t < T (lo = 2, hi = n - 2: the whole line)
+  constexpr int lo = 2;
+  const int T = n - 3;
+  int CH = (T + FINAL_NT - 1) / FINAL_NT;
+  CH |= 1;
+  const int t0 = tid * CH;
+  const int nq = ((t0 + CH < T) ? t0 + CH : T) - t0;
+  // this thread's samples y[lo + t0 - 1 .. lo + t0 + nq], loads issued together
+  double yv[FINAL_CHMAX + 2];
+#pragma unroll
+  for (int q = 0; q < FINAL_CHMAX + 2; q++) yv[q] = (q < nq + 2) ? y[lo + t0 - 1 + q] : 0.0;
+  __syncthreads();
+  const double M1 = S.m1, Mn1 = S.mn1;
+  const double BL = M1, BR = Mn1;
+  auto ct = [&](int t) { return S.ct[t < 16 ? t : 16]; };
+  double rr[FINAL_CHMAX], cc[FINAL_CHMAX], dd[FINAL_CHMAX];
+#pragma unroll
+  for (int q = 0; q < FINAL_CHMAX; q++) {
+    if (q < nq) {
+      const int t = t0 + q;
+      double r = 6.0 * ((yv[q + 2] - yv[q + 1]) - (yv[q + 1] - yv[q]));
+      if (t == 0) r -= BL;
+      if (t == T - 1) r -= BR;
+      rr[q] = r;
+      cc[q] = ct(t);
+    }
+  }
+  // forward sweep: d -> -c d + c r
+  double A = 1.0, B = 0.0;
+#pragma unroll
+  for (int q = 0; q < FINAL_CHMAX; q++) {
+    if (q < nq) {
+      const double c = cc[q];
+      A = -c * A;
+      B = (rr[q] - B) * c;
+    }
+  }
+  double dprev = block_affine_carry<FINAL_NT>(A, B, false, tid, S);
+#pragma unroll
+  for (int q = 0; q < FINAL_CHMAX; q++) {
+    if (q < nq) {
+      const double d = (rr[q] - dprev) * cc[q];
+      dd[q] = d;
+      dprev = d;
+    }
+  }
+  // back substitution: M -> d - c M, top down
+  A = 1.0; B = 0.0;
+#pragma unroll
+  for (int q = FINAL_CHMAX - 1; q >= 0; q--) {
+    if (q < nq) {
+      const double c = cc[q];
+      A = -c * A;
+      B = dd[q] - c * B;
+    }
+  }
+  double Mnext = block_affine_carry<FINAL_NT>(A, B, true, tid, S);
+  double* ms = S.ms;
+#pragma unroll
+  for (int q = FINAL_CHMAX - 1; q >= 0; q--) {
+    if (q < nq) {
+      const double M = dd[q] - cc[q] * Mnext;
+      ms[lo + t0 + q] = M;
+      Mnext = M;
+    }
+  }
+  __syncthreads();
+  if (tid == 0) {
+    ms[1] = M1;
+    ms[0] = 2.0 * M1 - ms[2];
+    ms[n - 1] = Mn1;
+    ms[n] = 2.0 * Mn1 - ms[n - 2];
+  }
+  __syncthreads();
+  // ---- evaluation at W points: linspace(b - ib, (e - b) + (b - ib), W + 1)[:-1]
+  const double x0 = begin - (double)ib;
+  const double span = end - begin;
+  const double step = ((span + x0) - x0) / (double)W;
+  const double wow = (end - begin) / (double)C.linelen;
   const bool pal = C.system == 1;
   const double scale_ = pal ? (double)(0xd300 - 0x0100) / (100 - C.vsync_ire)
                             : (double)(0xc800 - 0x0400) / (100 - C.vsync_ire);
   const double base = pal ? 256.0 : 1024.0;
-  // line geometry as spline_block checks it: samples y[0..n] = dm[ib .. ib + n]
-  auto geom = [&](int row, int64_t& ib, int& n) {
-    const int64_t b = py_int(lf[row + loff]), e = py_int(lf[row + loff + 1]);
-    const int64_t n64 = e - b;
-    ib = b;
-    n = (b < 0 || n64 < 6 || n64 >= SPL_MAXN || b + n64 + 1 > len) ? -1 : (int)n64;
-  };
-  double pre[FINAL_PF];
-  auto prefetch = [&](int row) {
-    int64_t ib;
-    int n;
-    geom(row, ib, n);
+  constexpr int NO = (MAX_OUTW + FINAL_NT - 1) / FINAL_NT;
+  double yk[NO], yk1[NO];
+  int kk[NO];
+  double xs[NO];
 #pragma unroll
-    for (int q = 0; q < FINAL_PF; q++) {
-      const int j = tid + FINAL_NT * q;
-      pre[q] = (j <= n) ? dm[ib + j] : 0.0;
-    }
-  };
-  prefetch(row0);
-  for (int row = row0; row < row1; row++) {
-    int64_t ib;
-    int n;
-    geom(row, ib, n);
-    __syncthreads();                           // the previous line's evaluation is done with S
-    if (n > 0) {
+  for (int e = 0; e < NO; e++) {
+    const int o = tid + FINAL_NT * e;
+    double x = (double)o * step;
+    x = x + x0;
+    int64_t j = (int64_t)floor(x);
+    const int k = (int)(j < 0 ? 0 : (j > n - 1 ? n - 1 : j));
+    kk[e] = k;
+    xs[e] = x;
+    yk[e] = (o < W) ? y[k] : 0.0;
+    yk1[e] = (o < W) ? y[k + 1] : 0.0;
+  }
 #pragma unroll
-      for (int q = 0; q < FINAL_PF; q++) {
-        const int j = tid + FINAL_NT * q;
-        if (j <= n) S.ys[j] = pre[q];
-      }
-    }
-    if (row + 1 < row1) prefetch(row + 1);
-    const int l = row + loff;
-    uint16_t* out = pic + (int64_t)slot * pic_stride + (int64_t)row * W;
-    const double b0 = lf[l], b1 = lf[l + 1];
-    const double wow = (b1 - b0) / (double)C.linelen;
-    const int rc = spline_block<FINAL_NT, 1, true>(dm, len, b0, b1, W, 0, W, tid, S, [&](int o, double v) {
-      double red = ((v * wow) - C.ire0) / C.hz_ire;
-      red -= C.vsync_ire;
-      double x = (red * scale_) + base;
-      if (x != x) x = 0.0;
-      x = fmin(fmax(x, 0.0), 65535.0) + 0.5;
-      out[o] = (uint16_t)x;
-    });
-    if (rc < 0) {
-      if (tid == 0) R->status = FS_TBC;
-      return;                                  // uniform: rc depends only on the line geometry
-    }
-    // NTSC burst flag pixels (threads 0 / 1 wrote pixels 0 / 1 above)
-    if (!pal && tid < 2 && row >= 1 && row < lc - 1) {
-      const float bl = blevel[(int64_t)slot * MAX_LINES + row];
-      const double hzs = 1700000 / 140.0;
-      if (tid == 0) out[0] = bl > 0 ? 16384 : 32768;
-      const double clevel = (1 / 1.45) / hzs;
-      if (tid == 1) out[1] = (uint16_t)(327.67 * clevel * fabs((double)bl));
-    }
+  for (int e = 0; e < NO; e++) {
+    const int o = tid + FINAL_NT * e;
+    if (o >= W) continue;
+    const double x = xs[e];
+    const int k = kk[e];
+    const double Mk = ms[k], Mk1 = ms[k + 1];
+    const double a = (double)(k + 1) - x, b = x - (double)k;
+    const double v = Mk * a * a * a / 6.0 + Mk1 * b * b * b / 6.0 + (yk[e] - Mk / 6.0) * a + (yk1[e] - Mk1 / 6.0) * b;
+    double red = ((v * wow) - C.ire0) / C.hz_ire;
+    red -= C.vsync_ire;
+    double px = (red * scale_) + base;
+    if (px != px) px = 0.0;
+    px = fmin(fmax(px, 0.0), 65535.0) + 0.5;
+    out[o] = (uint16_t)px;
+  }
+  // NTSC burst flag pixels (threads 0 / 1 wrote pixels 0 / 1 above)
+  if (!pal && tid < 2 && row >= 1 && row < lc - 1) {
+    const float bl = blevel[(int64_t)slot * MAX_LINES + row];
+    const double hzs = 1700000 / 140.0;
+    if (tid == 0) out[0] = bl > 0 ? 16384 : 32768;
+    const double clevel = (1 / 1.45) / hzs;
+    if (tid == 1) out[1] = (uint16_t)(327.67 * clevel * fabs((double)bl));
   }
 }
 
