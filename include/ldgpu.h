@@ -140,8 +140,9 @@ int ldg_set_capture(ldg_ctx* ctx, const void* data, int64_t nsamples, int fmt, i
 int ldg_decode_reads(ldg_ctx* ctx, int n, const int64_t* read_starts, const double* mtf, const int32_t* slots,
                      ldg_field_info* info);
 /* The same in two halves: launch without waiting, then wait and fetch the
- * records of the OLDEST outstanding call.  Up to two calls may be outstanding:
- * the second call's demod overlaps the first call's field kernels.  Slots of
+ * records of the OLDEST outstanding call.  Up to four calls may be outstanding:
+ * a call's demod overlaps the field kernels of the calls before it, and with
+ * three outstanding the demods run back to back.  Slots of
  * outstanding calls must be distinct and are not readable until their wait.
  * Output work (frames, audio, archive, comb) runs on other streams, so a host
  * can replay and output one batch while the next two decode. */

@@ -166,7 +166,10 @@ class GPUDecoder:
         self.sysp = self.rf.system
         self.batch = batch
         # two launches in flight + the batch the host replays + the cached path
-        self.capacity = capacity or max(4 * batch, batch + 16)
+        self.depth = int(os.environ.get('LDG_DEPTH', '2'))   # launches kept in flight (3 measured ~9% slower)
+        if not 1 <= self.depth <= 4:
+            raise ValueError('LDG_DEPTH must be 1..4')
+        self.capacity = capacity or max((self.depth + 2) * batch, batch + 16)
         self.ctx = native.Context(system, device, max_reads=self.capacity, max_frames=self.capacity)
         self.ctx.set_filters(self.rf.params(), self.rf.tables)
         self.log = log or (lambda *a: None)
@@ -184,7 +187,6 @@ class GPUDecoder:
         self.comb, self.comb_sink = False, None
         self.pending = []                  # (keys, slots) of the outstanding decode launches, oldest first
         self.inflight = set()              # keys of those launches
-        self.depth = int(os.environ.get('LDG_DEPTH', '2'))   # launches kept in flight in steady state
         self.transitions = []              # audio-offset chain: linecount of each transition's field
         self.archive, self.arch_next, self.shard_frames = False, 0, []
         self._out_pending = None           # (frames, pics, audio fields, sink) awaiting their audio

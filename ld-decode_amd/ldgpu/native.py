@@ -204,7 +204,7 @@ class Context:
         return list(info)
 
     def decode_reads_async(self, starts, mtfs, slots):
-        """Launch a decode (ldg_decode_reads_async, up to 2 outstanding); decode_reads_wait()
+        """Launch a decode (ldg_decode_reads_async, up to 4 outstanding); decode_reads_wait()
         returns the records of the oldest outstanding one."""
         s, m, sl = (np.ascontiguousarray(starts, dtype=np.int64), np.ascontiguousarray(mtfs, dtype=np.float64),
                     np.ascontiguousarray(slots, dtype=np.int32))

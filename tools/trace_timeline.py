@@ -30,6 +30,10 @@ def main(path, dump=0):
         (dem if k == 'ldg_k_demod' else other)[a:b] = True
     print('span %.1f ms: demod active %.1f, other only %.1f, idle %.1f' % (
         (t1 - t0) / 1e6, dem.sum() / 1e3, (other & ~dem).sum() / 1e3, (~dem & ~other).sum() / 1e3))
+    dm = sorted((s, e) for s, e, k, q in rows if k == 'ldg_k_demod')
+    if len(dm) > 2:
+        gaps = [(b[0] - a[1]) / 1e3 for a, b in zip(dm, dm[1:])]
+        print('demod-to-demod gap: median %.1f us, max %.1f us' % (np.median(gaps), max(gaps)))
     d = collections.defaultdict(list)
     for s, e, k, q in rows:
         d[k].append((e - s) / 1e3)
