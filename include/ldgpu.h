@@ -23,6 +23,8 @@
  *     lddecode_core.py:1238-1252
  *   comb-ntsc stdin/stdout frame stream, dim=2          ldg_comb_ntsc
  *     comb-ntsc.cxx:834-892, 1099-1117
+ *   comb-ntsc -d 3 -F [-c core] [-r range] (3D, no      ldg_comb_ntsc3d
+ *     optical flow) comb-ntsc.cxx:369-412, 834-892, 983-993, 1077-1082
  *
  * The Python host (ld-decode_amd/ldgpu) keeps readfield/readframe/mergevbi,
  * the read-position / MTF / audio-offset chains and the file writers, and
@@ -200,6 +202,17 @@ int ldg_comb_reset(ldg_ctx* ctx);
  * with the next ldg_decode_reads; the next ldg_assemble_frames into the
  * context buffer waits for it.  ldg_sync waits for all outstanding work. */
 int ldg_comb_ntsc_async(ldg_ctx* ctx, int n);
+/* 3D NTSC comb without optical flow, as `comb-ntsc -d 3 -F -c core -r range`
+ * (Process with f = 1 and Split3D(opt_flow = false), comb-ntsc.cxx:369-412,
+ * 834-892).  The reference combs frame k once frame k+1 has been read, so a
+ * process outputs nothing for its first two frames and never outputs its last
+ * one: this call takes n host frames, writes *n_out rgb48 frames to host
+ * rgb_out (room for n is enough) and holds the last two inputs in ctx for the
+ * next call.  core_ire / range_ire < 0 take the -F defaults 1.25 / 5.5 IRE.
+ * Shares the burst-level EMA with ldg_comb_ntsc (one process is either 2D or
+ * 3D); ldg_comb_reset also drops the held frames. */
+int ldg_comb_ntsc3d(ldg_ctx* ctx, int n, const uint16_t* frames, uint16_t* rgb_out, int* n_out, double core_ire,
+                    double range_ire);
 int ldg_sync(ldg_ctx* ctx);
 
 /* ---- in-library kernel timing (HIP events on the context's stream) ------------- */

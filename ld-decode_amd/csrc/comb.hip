@@ -1,4 +1,5 @@
-// 2D NTSC comb filter: .tbc frames (910 x 525 uint16, 4fsc) -> rgb48 744 x 480.
+// NTSC comb filter: .tbc frames (910 x 525 uint16, 4fsc) -> rgb48 744 x 480,
+// 2D (the default) or 3D without optical flow (comb-ntsc -d 3 -F).
 //
 // Restates comb-ntsc.cxx's default path (dim = 2, HQ colour LPF, nr_y = 1 IRE,
 // nr_c = 0, no pulldown): Comb::Process :834-892 -> Split1D :246-288, Split2D
@@ -12,6 +13,15 @@
 // (418 feeds each).  DoYNR's FIR history crosses lines and frames in the
 // reference, but for output pixels (x >= 78) all 25 taps fall inside the same
 // line (h - 12 >= 66 >= 40), so the history never reaches an output pixel.
+//
+// 3D (-d 3 -F): Process with f = 1 (:837,851-866) combs frame k once frame
+// k+1 has arrived; Split3D(opt_flow = false) :369-412 adds a temporal chroma
+// estimate clp2 = (prev + next)/2 - cur (integer average) with weight combk2
+// from the lp_3d-filtered |next - prev| of the line, and combk1 = 1 - combk2.
+// Only ldg_k_comb_split changes (ldg_k_comb_split3): the frames are passed as
+// a contiguous window, so frame k's neighbours are one frame before and after.
+// Split3D reads _k[4] and _k[832..835] without writing them (uninitialised
+// stack in the reference): build-defined 0 here and in the oracle.
 //
 // Three row kernels, so that no workgroup holds a CU's LDS while one lane
 // runs a 418-step chain:
@@ -42,6 +52,12 @@ constexpr double P_2DRANGE = 45 * IRESCALE;
 constexpr double LPI_B0 = 2.267438981796600e-01, LPI_B1 = 2.267438981796600e-01;
 constexpr double LPI_A1 = -5.465122036406802e-01;
 
+struct LP3DTaps { double b[17]; };   // lp_3d = fir1(16, 0.1), comb-ntsc.cxx:379
+__constant__ LP3DTaps g_lp3d = {{0.005719569452904, 0.009426612841315, 0.019748592575455, 0.036822680065252,
+                                 0.058983880135427, 0.082947830292278, 0.104489989820068, 0.119454688318951,
+                                 0.124812312996699, 0.119454688318952, 0.104489989820068, 0.082947830292278,
+                                 0.058983880135427, 0.036822680065252, 0.019748592575455, 0.009426612841315,
+                                 0.005719569452904}};
 struct NRTaps { double b[25]; };
 __constant__ NRTaps g_nr = {{
     1.141291975113614e-04, -1.857019211291029e-03, -4.499636864042073e-03, -5.577680979937061e-03,
@@ -185,10 +201,15 @@ extern "C" __global__ __launch_bounds__(256) void ldg_k_comb_burst(const uint16_
 
 // ---- ldg_k_comb_split: SplitIQ's signed chroma of one row.
 // grid: n * 480 workgroups of 256 threads; row r = line r + 38; cv: [n][480][CV_STRIDE].
-extern "C" __global__ __launch_bounds__(256) void ldg_k_comb_split(const uint16_t* __restrict__ frames,
-                                                                   double* __restrict__ cvbuf) {
+// D3: frames[f] has its neighbours at frames[f -+ 1] (core / range: p_3dcore,
+// p_3drange times irescale).
+template <bool D3>
+__device__ __forceinline__ void comb_split_row(const uint16_t* __restrict__ frames, double* __restrict__ cvbuf,
+                                               double core, double range) {
   __shared__ uint16_t s_raw[3][IN_X + 2];                // raw lines l-2, l, l+2
   __shared__ double s_c[3][IN_X];                        // Split1D clp0 of those lines
+  __shared__ uint16_t s_pn[D3 ? 2 : 1][IN_X + 2];        // 3D: line l of the previous / next frame
+  __shared__ double s_x[D3 ? IN_X : 1];                  // 3D: lp_3d's input __k (0 where not fed)
   const int tid = threadIdx.x;
   const int f = blockIdx.x / OUT_H;
   const int row = blockIdx.x % OUT_H;
@@ -201,7 +222,28 @@ extern "C" __global__ __launch_bounds__(256) void ldg_k_comb_split(const uint16_
     s_raw[k][2 * w] = (uint16_t)(v & 0xffff);
     s_raw[k][2 * w + 1] = (uint16_t)(v >> 16);
   }
+  if constexpr (D3) {
+    for (int t = tid; t < 2 * (IN_X / 2); t += 256) {
+      const int k = t / (IN_X / 2), w = t % (IN_X / 2);
+      const uint16_t* nb = fr + (k ? 1 : -1) * (ptrdiff_t)IN_X * IN_Y;   // k 0: previous, 1: next frame
+      const uint32_t v = reinterpret_cast<const uint32_t*>(nb + (size_t)l * IN_X)[w];
+      s_pn[k][2 * w] = (uint16_t)(v & 0xffff);
+      s_pn[k][2 * w + 1] = (uint16_t)(v >> 16);
+    }
+  }
   __syncthreads();
+  if constexpr (D3) {
+    // __k = |F0 - F2| + |(F1 - F2) - (F1 - F0)| (ints), fed to lp_3d for h = 13..839
+    for (int h = tid; h < IN_X; h += 256) {
+      double k = 0.0;
+      if (h > 12 && h < 840) {
+        const int p = s_pn[0][h], c = s_raw[1][h], nx = s_pn[1][h];
+        k = abs(nx - p);
+        k += abs((c - p) - (c - nx));
+      }
+      s_x[h] = k;
+    }
+  }
   for (int h = tid; h < IN_X; h += 256) {
 #pragma unroll
     for (int k = 0; k < 3; k++) {
@@ -221,13 +263,33 @@ extern "C" __global__ __launch_bounds__(256) void ldg_k_comb_split(const uint16_
     double cv = 0.0;
     if (h >= 4 && h < 840) {
       double cavg = 0;
-      cavg += 0.0 * 0.0;                                 // clpbuffer[2] * combk[2]
-      if (l < 524 && h >= 18) {
-        cavg += clp1_lds(s_c[0], s_c[1], s_c[2], h) * 1.0;
-        cavg += s_c[1][h] * 0.0;
+      if constexpr (D3) {
+        // _k[h] = lp_3d output of the feed at h + 8 (h = 5..831), the raw __k at
+        // 836..839, 0 at 4 and 832..835 (never written in the reference)
+        double kk = 0.0;
+        if (h >= 5 && h <= 831) {
+#pragma unroll
+          for (int t = 0; t < 17; t++) kk += (g_lp3d.b[t] / 1.0) * s_x[h + 8 - t];
+        } else if (h >= 836) {
+          kk = s_x[h];
+        }
+        const double k2 = clampd(1 - ((kk - core) / range), 0, 1);
+        const double k1 = 1 - k2;                        // lines 38..517 are all in [2, 523]
+        const double k0 = 1 - k2 - k1;
+        const double clp2 = (double)((((int)s_pn[1][h] + (int)s_pn[0][h]) / 2) - (int)s_raw[1][h]);
+        const double clp1 = (h >= 18) ? clp1_lds(s_c[0], s_c[1], s_c[2], h) : 0.0;
+        cavg += clp2 * k2;
+        cavg += clp1 * k1;
+        cavg += s_c[1][h] * k0;
       } else {
-        cavg += 0.0 * 0.0;
-        cavg += s_c[1][h] * 1.0;
+        cavg += 0.0 * 0.0;                               // clpbuffer[2] * combk[2]
+        if (l < 524 && h >= 18) {
+          cavg += clp1_lds(s_c[0], s_c[1], s_c[2], h) * 1.0;
+          cavg += s_c[1][h] * 0.0;
+        } else {
+          cavg += 0.0 * 0.0;
+          cavg += s_c[1][h] * 1.0;
+        }
       }
       cavg /= 2;
       if (!invertphase) cavg = -cavg;
@@ -235,6 +297,18 @@ extern "C" __global__ __launch_bounds__(256) void ldg_k_comb_split(const uint16_
     }
     cvrow[h] = cv;
   }
+}
+
+extern "C" __global__ __launch_bounds__(256) void ldg_k_comb_split(const uint16_t* __restrict__ frames,
+                                                                   double* __restrict__ cvbuf) {
+  comb_split_row<false>(frames, cvbuf, 0.0, 1.0);
+}
+
+// 3D (-d 3 -F): frames[-1] and frames[n] must be valid (the window's neighbours).
+extern "C" __global__ __launch_bounds__(256) void ldg_k_comb_split3(const uint16_t* __restrict__ frames,
+                                                                    double* __restrict__ cvbuf, double core,
+                                                                    double range) {
+  comb_split_row<true>(frames, cvbuf, core, range);
 }
 
 // ---- ldg_k_comb_iq: FilterIQ's two chains of every row with line >= 44, one

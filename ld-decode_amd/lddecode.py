@@ -10,7 +10,8 @@ bytes_per_frame and the fd.tell() + 1.05 frame EOF guard), `frame <n>` lines,
 and the same outputs: <outfile>.tbc (native uint16 frames) and <outfile>.pcm
 (int16 stereo, 48 kHz); cut mode (-c) writes <outfile>.r16.  Additions:
 <outfile>.json (per-frame VBI and per-field metadata, one JSON list) and
---comb (<outfile>.rgb: comb-ntsc's default rgb48 744x480 frames).
+--comb (<outfile>.rgb: comb-ntsc's default rgb48 744x480 frames; --comb-3d:
+comb-ntsc -d 3 -F's).  The comb alone, on a .tbc stream: comb_ntsc.py.
 """
 import argparse
 import json
@@ -42,6 +43,11 @@ def parse(argv=None):
     p.add_argument('--device', type=int, default=0, help='HIP device')
     p.add_argument('--batch', type=int, default=64, help='field reads per GPU launch')
     p.add_argument('--comb', action='store_true', help='also write <outfile>.rgb through the 2D NTSC comb')
+    p.add_argument('--comb-3d', action='store_true',
+                   help='with --comb: the 3D comb without optical flow (comb-ntsc -d 3 -F); '
+                        'every frame but the first and the last')
+    p.add_argument('--comb-3d-core', type=float, default=-1.0, help='comb-ntsc -c (IRE, default 1.25)')
+    p.add_argument('--comb-3d-range', type=float, default=-1.0, help='comb-ntsc -r (IRE, default 5.5)')
     p.add_argument('--no-json', action='store_true', help='do not write <outfile>.json')
     return p.parse_args(argv)
 
@@ -125,7 +131,8 @@ def main(argv=None):
 
     n = dec.decode(start_frame=firstframe, length=num_frames, sink=sink, comb=args.comb,
                    comb_sink=(lambda r: rgb.write(r.tobytes())) if rgb else None,
-                   start_sample=nextsample)
+                   start_sample=nextsample,
+                   comb3d=(args.comb_3d_core, args.comb_3d_range) if args.comb_3d else None)
     if req_frames is not None and n < req_frames:
         print('Warning: end of file reached before requested number of frames were decoded')
     tbc.close()

@@ -185,6 +185,7 @@ class GPUDecoder:
         self.field_nom = int(round(self.rf.freq_hz / self.sysp.fps / 2))
         self.trace = None          # diagnostics: planner steps (tools/miss_probe.py)
         self.comb, self.comb_sink = False, None
+        self.comb3d = None                 # (core_ire, range_ire): the 3D comb (comb-ntsc -d 3 -F)
         self.pending = []                  # (keys, slots) of the outstanding decode launches, oldest first
         self.inflight = set()              # keys of those launches
         self.transitions = []              # audio-offset chain: linecount of each transition's field
@@ -581,12 +582,15 @@ class GPUDecoder:
         return loader_tell(self.fmt, read_geometry(self.last_read)[2], self.cap_bytes)
 
     def decode(self, start_frame=0, length=None, sink=None, comb=False, comb_sink=None, start_sample=None,
-               stop_sample=None, keep_from=None, firstframe=True, archive=False, init_state=None):
+               stop_sample=None, keep_from=None, firstframe=True, archive=False, init_state=None, comb3d=None):
         """Decode frames; sink(frame_u16, pcm_i16, meta) per frame (None: frames stay in HBM).
 
         comb: also run the 2D NTSC comb (comb-ntsc.cxx dim=2) on every frame, in
         order, as one comb process; comb_sink(rgb48) receives each 480x744x3
-        frame (None with sink=None: the rgb frames stay in HBM).
+        frame (None with sink=None: the rgb frames stay in HBM).  comb3d = (core_ire,
+        range_ire) runs the 3D comb without optical flow instead (comb-ntsc -d 3 -F;
+        negative values: the -F defaults); it outputs every frame but the first and
+        the last, one frame late, and needs a sink.
         Field-group sharding (ldgpu/shard.py) hooks: start at start_sample; stop
         before a frame that would start at or after stop_sample; frames starting
         before keep_from are decoded (they lock the read / MTF chains) but not
@@ -595,7 +599,9 @@ class GPUDecoder:
         field archive instead of computing its 48 kHz audio (the shard's audio
         time offset is known only after the exchange), see self.shard_frames.
         Returns the number of frames decoded."""
-        self.comb, self.comb_sink = comb, comb_sink
+        self.comb, self.comb_sink, self.comb3d = comb, comb_sink, (comb3d if comb else None)
+        if self.comb3d is not None and sink is None:
+            raise ValueError('the 3D comb runs on host frames (a sink is required)')
         self.archive, self.arch_next, self.shard_frames = archive, 0, []
         self.transitions = []
         if comb:
@@ -708,7 +714,7 @@ class GPUDecoder:
         else:
             pics = self.ctx.assemble_frames(tops, bots, W, H)
             if self.comb:
-                rgb = self.ctx.comb_ntsc(pics)
+                rgb = self.ctx.comb_ntsc(pics) if self.comb3d is None else self.ctx.comb_ntsc3d(pics, *self.comb3d)
                 if self.comb_sink:
                     for r in rgb:
                         self.comb_sink(r)

@@ -22,7 +22,7 @@ EXPORTS = ['ldg_create', 'ldg_destroy', 'ldg_last_error', 'ldg_set_filters', 'ld
            'ldg_comb_ntsc', 'ldg_comb_reset', 'ldg_version', 'ldg_device_count', 'ldg_profile_enable',
            'ldg_profile_read', 'ldg_synth_capture', 'ldg_capture_download', 'ldg_comb_ntsc_async', 'ldg_sync',
            'ldg_archive_fields', 'ldg_archive_audio', 'ldg_decode_reads_async', 'ldg_decode_reads_wait',
-           'ldg_field_audio_async', 'ldg_field_audio_collect']
+           'ldg_field_audio_async', 'ldg_field_audio_collect', 'ldg_comb_ntsc3d']
 
 
 class FieldInfo(C.Structure):
@@ -100,6 +100,7 @@ def load(path=None):
     lib.ldg_comb_ntsc.argtypes = [vp, C.c_int, vp, vp, C.c_int]
     lib.ldg_comb_reset.argtypes = [vp]
     lib.ldg_comb_ntsc_async.argtypes = [vp, C.c_int]
+    lib.ldg_comb_ntsc3d.argtypes = [vp, C.c_int, vp, vp, C.POINTER(C.c_int), C.c_double, C.c_double]
     lib.ldg_decode_reads_async.argtypes = [vp, C.c_int, vp, vp, vp]
     lib.ldg_decode_reads_wait.argtypes = [vp, vp]
     lib.ldg_archive_fields.argtypes = [vp, C.c_int, vp, C.c_int64]
@@ -298,6 +299,17 @@ class Context:
         self._check(self.lib.ldg_comb_ntsc(self.h, f.shape[0], f.ctypes.data_as(C.c_void_p),
                                            out.ctypes.data_as(C.c_void_p), 0), 'ldg_comb_ntsc')
         return out
+
+    def comb_ntsc3d(self, frames, core_ire=-1.0, range_ire=-1.0):
+        """3D NTSC comb without optical flow (comb-ntsc -d 3 -F): n x (525, 910) uint16 frames in,
+        the rgb48 frames that now have both neighbours out (none for a process's first two frames)."""
+        f = np.ascontiguousarray(frames, dtype=np.uint16).reshape(-1, 525 * 910)
+        out = np.zeros((f.shape[0], 480, 744, 3), dtype=np.uint16)
+        n_out = C.c_int(0)
+        self._check(self.lib.ldg_comb_ntsc3d(self.h, f.shape[0], f.ctypes.data_as(C.c_void_p),
+                                             out.ctypes.data_as(C.c_void_p), C.byref(n_out), core_ire, range_ire),
+                    'ldg_comb_ntsc3d')
+        return out[:n_out.value]
 
     def comb_ntsc_device(self, n):
         """Comb the first n frames of the context's device frame buffer (ldg_assemble_frames

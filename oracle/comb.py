@@ -1,5 +1,6 @@
 """ORACLE -- test infrastructure only.  ctypes wrapper of oracle/comb2d.cpp, the
-C++ restatement of the reference NTSC 2D comb (comb-ntsc.cxx dim=2 defaults).
+C++ restatement of the reference NTSC comb (comb-ntsc.cxx dim=2 defaults, and
+the non-optical-flow 3D path -d 3 -F).
 Built by oracle/Makefile into oracle/_build/libcomb2d.so."""
 import ctypes as C
 import os
@@ -21,6 +22,12 @@ def _load():
     lib.comb2d_process.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p]
     lib.comb2d_aburstlev.argtypes = [C.c_void_p]
     lib.comb2d_aburstlev.restype = C.c_double
+    lib.comb3d_create.restype = C.c_void_p
+    lib.comb3d_destroy.argtypes = [C.c_void_p]
+    lib.comb3d_process.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_double, C.c_double]
+    lib.comb3d_process.restype = C.c_int
+    lib.comb3d_aburstlev.argtypes = [C.c_void_p]
+    lib.comb3d_aburstlev.restype = C.c_double
     return lib
 
 
@@ -45,3 +52,28 @@ class Comb2D:
     @property
     def aburstlev(self):
         return self.lib.comb2d_aburstlev(self.h)
+
+
+class Comb3D:
+    """One reference comb process run as `comb-ntsc -d 3 -F [-c core] [-r range]`:
+    frame k is output once frame k+1 has arrived (none for the first two inputs)."""
+
+    def __init__(self, core_ire=-1.0, range_ire=-1.0):
+        self.lib = _load()
+        self.h = self.lib.comb3d_create()
+        self.core, self.range = core_ire, range_ire
+
+    def __del__(self):
+        if getattr(self, 'h', None):
+            self.lib.comb3d_destroy(self.h)
+            self.h = None
+
+    def process(self, frames):
+        f = np.ascontiguousarray(frames, dtype=np.uint16).reshape(-1, IN_Y, IN_X)
+        out = np.zeros((f.shape[0], OUT_H, OUT_W, 3), dtype=np.uint16)
+        n = self.lib.comb3d_process(self.h, f.shape[0], f.ctypes.data, out.ctypes.data, self.core, self.range)
+        return out[:n]
+
+    @property
+    def aburstlev(self):
+        return self.lib.comb3d_aburstlev(self.h)

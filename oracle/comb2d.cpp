@@ -1,6 +1,7 @@
 // ORACLE -- TEST INFRASTRUCTURE ONLY.  C++ restatement of the reference NTSC
 // comb filter's default path (comb-ntsc.cxx, dim = 2, no pulldown, 16-bit
-// output) used as the checker for the GPU comb.  PARITY UNPINNED against the
+// output) and of its non-optical-flow 3D path (-d 3 -F), used as the checker
+// for the GPU comb.  PARITY UNPINNED against the
 // reference binary itself (running it is denied; it also needs
 // OpenCV, absent here); pinned by known-answer tests in tests/test_comb.py.
 //
@@ -18,10 +19,19 @@
 //   DoCNR                           :485-521   (nr_c = 0: no-op)
 //   ToRGB / RGB::conv / u16_to_ire  :555-598, :124-147, :116-121
 //   PostProcess + WriteFrame        :894-938, :704-733 (rows 38..517, x 78..821)
+//   3D (-d 3 -F): Process with f = 1 :837,851-866 (no output for the first two
+//   frames; frame k is combed with frames k-1 and k+1 once k+1 arrives),
+//   Split3D(opt_flow = false)       :369-412   (clp2, combk2 from the lp_3d-filtered
+//                                               frame difference; combk1 = 1 - combk2)
+//   p_3dcore / p_3drange defaults   :1077-1082 (1.25 / 5.5 IRE, times irescale)
+//   Build-defined (parity unpinned): Split3D reads _k[4] and _k[832..835],
+//   which it never writes (uninitialised stack in the reference); here 0.
 //   Filter::feed (DF-I order)       ld-decoder.h:167-214
 //   f_nr, f_colorlpi constants      deemp.h:367-380, :425-432
 #include <cmath>
 #include <cstdint>
+#include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -43,6 +53,12 @@ const double NR_B[25] = {
     1.098965697652803e-03,  3.029931283148557e-02,  2.861211356202848e-02,  1.309163063177156e-02,
     -4.423694440267185e-04, -5.577680979937061e-03, -4.499636864042074e-03, -1.857019211291030e-03,
     1.141291975113614e-04};
+// Split3D's lp_3d (fir1(16, 0.1), comb-ntsc.cxx:379)
+const double LP3D_B[17] = {0.005719569452904, 0.009426612841315, 0.019748592575455, 0.036822680065252,
+                           0.058983880135427, 0.082947830292278, 0.104489989820068, 0.119454688318951,
+                           0.124812312996699, 0.119454688318952, 0.104489989820068, 0.082947830292278,
+                           0.058983880135427, 0.036822680065252, 0.019748592575455, 0.009426612841315,
+                           0.005719569452904};
 // deemp.h f_colorlpi (1-pole IIR; the HQ default uses it for I and Q)
 constexpr double LPI_B0 = 2.267438981796600e-01, LPI_B1 = 2.267438981796600e-01;
 constexpr double LPI_A1 = -5.465122036406802e-01;
@@ -71,7 +87,10 @@ struct Comb {
     return y0;
   }
 
-  void process(const uint16_t* raw, uint16_t* rgb) {
+  // prev / next: the frames before and after `raw` for the 3D path (-d 3 -F),
+  // null for 2D; core / range: p_3dcore / p_3drange (already times irescale)
+  void process(const uint16_t* raw, uint16_t* rgb, const uint16_t* prev = nullptr, const uint16_t* next = nullptr,
+               double core = 0, double range = 1) {
     // ---- Split1D: clp0 (lines 44..524), combk0 = 1 there
     static double clp0[IN_Y + 2][IN_X], clp1[IN_Y][IN_X], k0[IN_Y][IN_X], k1[IN_Y][IN_X];
     std::memset(clp0, 0, sizeof(clp0));
@@ -125,6 +144,36 @@ struct Comb {
         k0[l][h] = 1 - 0.0 - k1[l][h];
       }
     }
+    // ---- Split3D (opt_flow = false; lines 36..524, h 4..839): Frame[0] = next,
+    //      Frame[1] = raw, Frame[2] = prev
+    static double clp2[IN_Y][IN_X], k2[IN_Y][IN_X];
+    std::memset(clp2, 0, sizeof(clp2));
+    std::memset(k2, 0, sizeof(k2));
+    if (prev) {
+      for (int l = 36; l < IN_Y; l++) {
+        const int o = l * IN_X;
+        double x[IN_X] = {0}, kk[IN_X] = {0};   // __k fed at h = 13..839; _k[4], _k[832..835] stay 0
+        for (int h = 4; h < 840; h++) {
+          const int adr = o + h;
+          double k = std::abs((int)next[adr] - (int)prev[adr]);
+          k += std::abs(((int)raw[adr] - (int)prev[adr]) - ((int)raw[adr] - (int)next[adr]));
+          if (h > 12) x[h] = k;
+          if (h >= 836) kk[h] = k;
+        }
+        for (int j = 5; j <= 831; j++) {       // _k[h - 8] = lp_3d.feed(__k(h)), h = 13..839
+          double y0 = 0;
+          for (int t = 0; t < 17; t++) y0 += (LP3D_B[t] / 1.0) * x[j + 8 - t];
+          kk[j] = y0;
+        }
+        for (int h = 4; h < 840; h++) {
+          const int adr = o + h;
+          clp2[l][h] = (double)((((int)next[adr] + (int)prev[adr]) / 2) - (int)raw[adr]);
+          k2[l][h] = clampd(1 - ((kk[h] - core) / range), 0, 1);
+          if (l >= 2 && l <= 523) k1[l][h] = 1 - k2[l][h];
+          k0[l][h] = 1 - k2[l][h] - k1[l][h];
+        }
+      }
+    }
     // ---- SplitIQ -> cbuf (lines 36..524; everything else zero)
     static YIQ cb[IN_Y][IN_X];
     std::memset(cb, 0, sizeof(cb));
@@ -134,7 +183,7 @@ struct Comb {
       double si = 0, sq = 0;
       for (int h = 4; h < 840; h++) {
         double cavg = 0;
-        cavg += 0.0 * 0.0;               // clpbuffer[2] * combk[2]
+        cavg += clp2[l][h] * k2[l][h];   // clpbuffer[2] * combk[2] (0 in 2D)
         cavg += clp1[l][h] * k1[l][h];
         cavg += clp0[l][h] * k0[l][h];
         cavg /= 2;
@@ -246,4 +295,36 @@ void comb2d_process(void* c, int n, const uint16_t* frames, uint16_t* rgb) {
     cb->process(frames + (size_t)f * IN_X * IN_Y, rgb + (size_t)f * OUT_W * OUT_H * 3);
 }
 double comb2d_aburstlev(void* c) { return static_cast<Comb*>(c)->aburstlev; }
+
+// One reference process in -d 3 -F mode: its own Comb state plus the last two
+// input frames.  Feeds n frames and writes one rgb48 frame per frame that now
+// has both neighbours (n + history - 2 of them, >= 0); returns that count.
+struct Comb3 {
+  Comb c;
+  std::vector<uint16_t> hist;   // up to 2 frames, oldest first
+  int nhist = 0;
+};
+void* comb3d_create() { return new Comb3(); }
+void comb3d_destroy(void* c) { delete static_cast<Comb3*>(c); }
+int comb3d_process(void* h, int n, const uint16_t* frames, uint16_t* rgb, double core_ire, double range_ire) {
+  Comb3* c = static_cast<Comb3*>(h);
+  const size_t F = (size_t)IN_X * IN_Y;
+  const double core = (core_ire < 0 ? 1.25 : core_ire) * IRESCALE;
+  const double range = (range_ire < 0 ? 5.5 : range_ire) * IRESCALE;
+  std::vector<uint16_t> win((size_t)(c->nhist + n) * F);
+  std::copy(c->hist.begin(), c->hist.begin() + (size_t)c->nhist * F, win.begin());
+  std::copy(frames, frames + (size_t)n * F, win.begin() + (size_t)c->nhist * F);
+  const int L = c->nhist + n;
+  int out = 0;
+  for (int k = 1; k + 1 < L; k++) {
+    c->c.process(&win[(size_t)k * F], rgb + (size_t)out * OUT_W * OUT_H * 3, &win[(size_t)(k - 1) * F],
+                 &win[(size_t)(k + 1) * F], core, range);
+    out++;
+  }
+  const int keep = L < 2 ? L : 2;
+  c->hist.assign(win.begin() + (size_t)(L - keep) * F, win.end());
+  c->nhist = keep;
+  return out;
+}
+double comb3d_aburstlev(void* c) { return static_cast<Comb3*>(c)->c.aburstlev; }
 }

@@ -123,3 +123,45 @@ def test_cli_sharded_two_ranks_equal_single(tmp_path):
     for ext in ('.tbc', '.pcm'):
         assert (tmp_path / ('one' + ext)).read_bytes() == (tmp_path / ('two' + ext)).read_bytes(), ext
     assert json.load(open(tmp_path / 'one.json')) == json.load(open(tmp_path / 'two.json'))
+
+
+COMB_CLI = os.path.join(ROOT, 'ld-decode_amd', 'comb_ntsc.py')
+
+
+def test_comb_cli_rejects_optical_flow_3d():
+    r = subprocess.run([sys.executable, COMB_CLI, '-d', '3'], capture_output=True, text=True, timeout=120,
+                       stdin=subprocess.DEVNULL)
+    assert r.returncode == 1 and 'use -d 3 -F' in r.stderr
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('dim', [2, 3])
+def test_comb_cli_stream_matches_oracle(tmp_path, dim):
+    """comb_ntsc.py as comb-ntsc's stdin/stdout filter (2D default, or -d 3 -F), with a
+    trailing partial frame that ends the stream (comb-ntsc.cxx:1102-1116)."""
+    sys.path.insert(0, HERE)
+    from test_comb import frames_3d
+    from oracle.comb import Comb2D, Comb3D
+    fr = frames_3d(seed=5, n=5)
+    data = fr.tobytes() + b'\x01' * 1000
+    args = [sys.executable, COMB_CLI, '--chunk', '2'] + (['-d', '3', '-F'] if dim == 3 else [])
+    r = subprocess.run(args, input=data, capture_output=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-2000:]
+    got = np.frombuffer(r.stdout, dtype=np.uint16).reshape(-1, 480, 744, 3)
+    exp = Comb2D().process(fr) if dim == 2 else Comb3D().process(fr)
+    assert got.shape == exp.shape
+    assert np.abs(got.astype(np.int64) - exp.astype(np.int64)).max() <= 1
+
+
+@pytest.mark.gpu
+def test_cli_comb_3d(tmp_path):
+    cap, gold = _golden_capture(tmp_path)
+    out = tmp_path / 'out'
+    r = run_cli('--comb', '--comb-3d', cap, out)
+    assert r.returncode == 0, r.stderr[-2000:]
+    frames = np.fromfile(str(out) + '.tbc', dtype=np.uint16).reshape(-1, 525, 910)
+    rgb = np.fromfile(str(out) + '.rgb', dtype=np.uint16).reshape(-1, 480, 744, 3)
+    assert len(rgb) == len(frames) - 2
+    from oracle.comb import Comb3D
+    o = Comb3D().process(frames)
+    assert np.abs(o.astype(np.int64) - rgb.astype(np.int64)).max() <= 1

@@ -140,3 +140,113 @@ def test_gpu_comb_on_decoded_frames():
     assert np.abs(g.astype(np.int64) - o.astype(np.int64)).max() <= 1
     exact = sum(hashlib.sha256(x.tobytes()).hexdigest() == e['comb_rgb48_sha256'] for x, e in zip(g, gold['frames']))
     print('comb: %d/%d frames bit-identical to golden' % (exact, len(g)))
+
+
+# ---- 3D comb without optical flow (comb-ntsc -d 3 -F) ---------------------------------
+
+from oracle.comb import Comb3D  # noqa: E402
+
+
+def test_oracle3d_frame_delay_and_chunking():
+    """Process with f = 1 (:837,860-868): nothing for the first two frames, frame k once
+    frame k+1 is in; the held frames carry across calls like one process."""
+    rng = np.random.default_rng(3)
+    fr = np.stack([np.clip(frame_solid(40.0 + 5 * k, 900, -500).astype(np.int64)
+                           + rng.integers(-200, 200, (525, 910)), 0, 65535).astype(np.uint16) for k in range(6)])
+    fr[:, :, :2] = frame_solid(40.0)[:, :2]
+    one = Comb3D().process(fr)
+    assert one.shape[0] == 4
+    c = Comb3D()
+    parts = [c.process(fr[:1]), c.process(fr[1:2]), c.process(fr[2:5]), c.process(fr[5:])]
+    assert [p.shape[0] for p in parts] == [0, 0, 3, 1]
+    assert np.array_equal(one, np.concatenate(parts))
+    # the first output is frame 1 combed with frames 0 and 2
+    assert np.array_equal(one[0], Comb3D().process(fr[:3])[0])
+
+
+@pytest.mark.parametrize('y_ire,a,b', [(40.0, 1500, -900), (60.0, -700, 1200)])
+def test_oracle3d_solid_colour_kat(y_ire, a, b):
+    """Real NTSC: the 4fsc chroma inverts from frame to frame.  With the neighbours
+    inverted, |next - prev| = 0, so combk2 = 1 and the temporal estimate
+    (prev + next)/2 - cur = -2c alone decodes the same I = -a, Q = b as the 2D KAT."""
+    f, g = frame_solid(y_ire, a, b), frame_solid(y_ire, -a, -b)
+    out = Comb3D().process(np.stack([g, f, g]))[0].astype(np.float64)
+    core = out[40:440, 100:700].reshape(-1, 3)
+    assert np.abs(core - np.floor(expected_rgb(y_ire, -a, b))).max() <= 1
+
+
+def test_oracle3d_static_scene_has_no_chroma():
+    """A frame repeated without the frame-to-frame inversion: the temporal estimate
+    is 0 with full weight, so I = Q = 0 and every output pixel is grey."""
+    f = frame_solid(50.0, 1200, 600)
+    out = Comb3D().process(np.stack([f, f, f]))[0].astype(np.int64)
+    core = out[10:470, 20:720]
+    assert (core[..., 0] == core[..., 1]).all() and (core[..., 1] == core[..., 2]).all()
+
+
+def test_oracle3d_motion_falls_back_to_2d():
+    """Neighbours that differ by far more than p_3dcore + p_3drange give combk2 = 0 and
+    combk1 = 1: away from the line ends the 3D output is the 2D output."""
+    f = frame_solid(50.0, 1000, -400)
+    prev, nxt = frame_solid(0.0, -1000, 400), frame_solid(100.0, -1000, 400)
+    three = Comb3D().process(np.stack([prev, f, nxt]))[0].astype(np.int64)
+    two = Comb2D().process(f[None])[0].astype(np.int64)
+    assert np.abs(three[:, 40:700] - two[:, 40:700]).max() <= 1
+
+
+def frames_3d(seed=11, n=7):
+    """Alternating-phase colour frames with noise, a moving luma edge and a cut."""
+    rng = np.random.default_rng(seed)
+    out = []
+    for k in range(n):
+        s = 1 if k % 2 == 0 else -1
+        fr = frame_solid(45.0 + (30.0 if k == 4 else 0.0), s * 1100, -s * 600).astype(np.int64)
+        fr[:, 200 + 40 * k:260 + 40 * k] += 9000
+        fr += rng.integers(-250, 250, (525, 910))
+        fr[:, :2] = frame_solid(45.0, burst_ire=20.0 + k)[:, :2]
+        out.append(np.clip(fr, 0, 65535).astype(np.uint16))
+    return np.stack(out)
+
+
+@pytest.mark.gpu
+def test_gpu_comb3d_matches_oracle(gpu_ctx_ntsc):
+    ctx, _ = gpu_ctx_ntsc
+    fr = frames_3d()
+    ctx.comb_reset()
+    parts = [ctx.comb_ntsc3d(fr[:1]), ctx.comb_ntsc3d(fr[1:4]), ctx.comb_ntsc3d(fr[4:])]
+    assert [p.shape[0] for p in parts] == [0, 2, 3]
+    g = np.concatenate(parts)
+    o = Comb3D().process(fr)
+    assert g.shape == o.shape
+    d = np.abs(g.astype(np.int64) - o.astype(np.int64))
+    assert d.max() <= 1, d.max()
+    assert (d > 0).mean() < 1e-3
+    # non-default -c / -r
+    ctx.comb_reset()
+    g2 = ctx.comb_ntsc3d(fr, 0.5, 2.0)
+    o2 = Comb3D(0.5, 2.0).process(fr)
+    assert np.abs(g2.astype(np.int64) - o2.astype(np.int64)).max() <= 1
+    ctx.comb_reset()
+
+
+@pytest.mark.gpu
+def test_gpu_comb3d_on_decoded_frames():
+    """RF -> .tbc on the GPU -> 3D comb on the GPU, against the oracle's 3D comb of the
+    same frames (+-1 LSB)."""
+    import os
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    sys.path.insert(0, os.path.join(here, 'golden'))
+    import make_golden
+    from ldgpu.decoder import GPUDecoder
+    dec = GPUDecoder(system='NTSC', batch=8)
+    dec.set_capture(make_golden.build_capture('ntsc_cav_u8_0p2s'), 0)
+    frames = []
+    dec.decode(sink=lambda fr, au, m: frames.append(fr.copy()))
+    fr = np.stack(frames).reshape(-1, 525, 910)
+    assert fr.shape[0] >= 3
+    dec.ctx.comb_reset()
+    g = dec.ctx.comb_ntsc3d(fr)
+    o = Comb3D().process(fr)
+    assert g.shape[0] == fr.shape[0] - 2
+    assert np.abs(g.astype(np.int64) - o.astype(np.int64)).max() <= 1
