@@ -23,6 +23,8 @@
  *     lddecode_core.py:1238-1252
  *   comb-ntsc stdin/stdout frame stream, dim=2          ldg_comb_ntsc
  *     comb-ntsc.cxx:834-892, 1099-1117
+ *   cx-expander stdin/stdout (.pcm post-chain)          ldg_cx_process
+ *     cx-expander.cxx:34-117
  *   comb-ntsc -d 3 -F [-c core] [-r range] (3D, no      ldg_comb_ntsc3d
  *     optical flow) comb-ntsc.cxx:369-412, 834-892, 983-993, 1077-1082
  *
@@ -245,6 +247,18 @@ int ldg_synth_capture(ldg_ctx* ctx, const ldg_synth_params* p, const double* fir
                       const uint32_t* codes, int64_t ncodeframes);
 /* Copy nbytes of the resident capture starting at byte offset to host dst. */
 int64_t ldg_capture_download(ldg_ctx* ctx, void* dst, int64_t offset, int64_t nbytes);
+
+/* CX expander for the .pcm stream (cx-expander.cxx:9-117): host code, one
+ * sequential chain (the channels are coupled through the peak followers).
+ * ldg_cx_process takes n stereo frames of uint16 (L, R interleaved; the
+ * reference reads the stream as unsigned and subtracts 32768) and writes n
+ * expanded stereo frames; state persists across calls like one cx process.
+ * The reference drops a trailing partial 1024-frame block (:105-113): that is
+ * the caller's (cx_expander.py's) job. */
+typedef struct ldg_cx ldg_cx;
+int ldg_cx_create(ldg_cx** out);
+int ldg_cx_destroy(ldg_cx* cx);
+int ldg_cx_process(ldg_cx* cx, int64_t n, const uint16_t* in, uint16_t* out);
 
 /* Library / device identification. */
 const char* ldg_version(void);

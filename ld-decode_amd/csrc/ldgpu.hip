@@ -5,3 +5,4 @@
 #include "comb.hip"
 #include "synth.hip"
 #include "abi.inc"
+#include "cx.inc"

@@ -22,7 +22,7 @@ EXPORTS = ['ldg_create', 'ldg_destroy', 'ldg_last_error', 'ldg_set_filters', 'ld
            'ldg_comb_ntsc', 'ldg_comb_reset', 'ldg_version', 'ldg_device_count', 'ldg_profile_enable',
            'ldg_profile_read', 'ldg_synth_capture', 'ldg_capture_download', 'ldg_comb_ntsc_async', 'ldg_sync',
            'ldg_archive_fields', 'ldg_archive_audio', 'ldg_decode_reads_async', 'ldg_decode_reads_wait',
-           'ldg_field_audio_async', 'ldg_field_audio_collect', 'ldg_comb_ntsc3d']
+           'ldg_field_audio_async', 'ldg_field_audio_collect', 'ldg_comb_ntsc3d', 'ldg_cx_create', 'ldg_cx_destroy', 'ldg_cx_process']
 
 
 class FieldInfo(C.Structure):
@@ -112,6 +112,9 @@ def load(path=None):
                                       C.POINTER(C.c_uint32), C.c_int64]
     lib.ldg_capture_download.argtypes = [vp, vp, C.c_int64, C.c_int64]
     lib.ldg_capture_download.restype = C.c_int64
+    lib.ldg_cx_create.argtypes = [C.POINTER(vp)]
+    lib.ldg_cx_destroy.argtypes = [vp]
+    lib.ldg_cx_process.argtypes = [vp, C.c_int64, vp, vp]
     lib.ldg_version.restype = C.c_char_p
     lib.ldg_device_count.restype = C.c_int
     _lib = lib
@@ -358,3 +361,28 @@ class Context:
         if n < 0:
             raise LDGError('ldg_capture_download -> %d' % n)
         return a[:n]
+
+
+class CXExpander:
+    """cx-expander (cx-expander.cxx:34-92) through ldg_cx_process: host code, no device needed.
+    State carries across process() calls like one cx process."""
+
+    def __init__(self):
+        self.lib = load()
+        h = C.c_void_p()
+        if self.lib.ldg_cx_create(C.byref(h)) != LDG_OK:
+            raise LDGError('ldg_cx_create failed')
+        self.h = h
+
+    def process(self, stereo_u16):
+        """(n, 2) or flat interleaved uint16 -> (n, 2) uint16."""
+        a = np.ascontiguousarray(stereo_u16, dtype=np.uint16).reshape(-1, 2)
+        out = np.empty_like(a)
+        if self.lib.ldg_cx_process(self.h, a.shape[0], a.ctypes.data, out.ctypes.data) != LDG_OK:
+            raise LDGError('ldg_cx_process failed')
+        return out
+
+    def __del__(self):
+        if getattr(self, 'h', None):
+            self.lib.ldg_cx_destroy(self.h)
+            self.h = None
