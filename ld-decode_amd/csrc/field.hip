@@ -198,6 +198,7 @@ extern "C" __global__ __launch_bounds__(64) void ldg_k_sync(
   const int64_t len = rd.n_out;
   const int linelen = C.linelen;
   const WalkGeom G(len, linelen);
+  KSTAMP(3, 0);
 
   // ---- get_syncpeaks, part 2: stitch the segment chains ------------------------
   for (int q = lane; q < SEG_K; q += 64) s_cnt[q] = node_n[(int64_t)slot * SEG_K + q];
@@ -206,7 +207,12 @@ extern "C" __global__ __launch_bounds__(64) void ldg_k_sync(
     s_npk[q] = node_pk[(int64_t)slot * SEG_K * SEG_NMAX + q];
   }
   __syncthreads();
+  KSTAMP(3, 1);
   const double* nlv = node_lv + (int64_t)slot * SEG_K * SEG_NMAX;
+  // the walk's peak levels are gathered after the stitch, all at once: here each
+  // peak records where its level is (node index, or -1 when the direct walk
+  // below already stored it), so no global load sits on the stitch's serial path
+  int32_t* s_lvi = s_cand;                 // s_cand is not used until the vsync candidates
   int np = 0;
   bool overflow = false;
   // append path nodes [a, b) of chain k (their peaks, in order)
@@ -218,7 +224,7 @@ extern "C" __global__ __launch_bounds__(64) void ldg_k_sync(
       const int rank = __popcll(m & ((1ull << lane) - 1ull));
       const int tot = __popcll(m);
       if (np + tot > MAX_PEAKS) { overflow = true; break; }
-      if (isp) { s_pk[np + rank] = s_npk[k * SEG_NMAX + j]; s_lv[np + rank] = nlv[k * SEG_NMAX + j]; }
+      if (isp) { s_pk[np + rank] = s_npk[k * SEG_NMAX + j]; s_lvi[np + rank] = k * SEG_NMAX + j; }
       np += tot;
     }
   };
@@ -267,7 +273,7 @@ extern "C" __global__ __launch_bounds__(64) void ldg_k_sync(
         tile_argmax(ds, stiles + (int64_t)slot * STILE_PER_SLOT, p, p + G.win, lane, best, bidx);
         if (best > .2) {
           if (np >= MAX_PEAKS) { overflow = true; break; }
-          if (lane == 0) { s_pk[np] = (int32_t)bidx; s_lv[np] = best; }
+          if (lane == 0) { s_pk[np] = (int32_t)bidx; s_lv[np] = best; s_lvi[np] = -1; }
           np++;
           p = bidx + G.jump;
         } else {
@@ -278,6 +284,10 @@ extern "C" __global__ __launch_bounds__(64) void ldg_k_sync(
     }
   }
   __syncthreads();
+  for (int q = lane; q < np; q += 64)
+    if (s_lvi[q] >= 0) s_lv[q] = nlv[s_lvi[q]];
+  __syncthreads();
+  KSTAMP(3, 2);
   if (lane == 0) R->npeaks = np;
   for (int k = lane; k < np; k += 64) peaks[(int64_t)slot * MAX_PEAKS + k] = s_pk[k];
   if (overflow) {
@@ -309,9 +319,12 @@ extern "C" __global__ __launch_bounds__(64) void ldg_k_sync(
     } else {
       med = __builtin_nan("");
     }
-    // np.std over the list in peak order (numpy pairwise order, lane 0)
-    if (lane == 0) s_sd = nh > 0 ? np_std(s_tmp, nh, s_tmp + nh) : __builtin_nan("");
+    // np.std over the list in peak order (numpy's pairwise order, on the wave)
+    KSTAMP(3, 3);
+    const double sdv = nh > 0 ? wave_np_std(s_tmp, nh, s_tmp + nh, lane) : __builtin_nan("");
+    if (lane == 0) s_sd = sdv;
     __syncthreads();
+    KSTAMP(3, 4);
     const double sd = s_sd;
     const double t2 = sd * 2;
     tol = (.01 > t2) ? .01 : t2;                     // Python max(t2, .01): keeps t2 unless .01 > t2
@@ -324,6 +337,7 @@ extern "C" __global__ __launch_bounds__(64) void ldg_k_sync(
       ncand += __popcll(m);
     }
     __syncthreads();
+    KSTAMP(3, 5);
   }
   if (lane != 0) return;
   if (np >= 200) {

@@ -62,6 +62,45 @@ __device__ inline double np_std(const double* a, int n, double* tmp) {
   return sqrt(pw_sum(tmp, n) / (double)n);
 }
 
+// pw_sum on one wave, result in every lane.  numpy's recursion splits n at
+// (n/2 rounded down to a multiple of 8) until a piece has <= 128 elements; the
+// pieces (at most 64 here) are summed one per lane with pw_block, then the
+// recursion is replayed with each piece's sum fetched from its lane, so every
+// addition happens in numpy's order.  Wave-uniform control flow throughout.
+template <int L> __device__ inline void pw_leaves(int off, int n, int& cnt, int lane, int& my_off, int& my_n) {
+  if (L == 0 || n <= 128) {
+    if (cnt == lane) { my_off = off; my_n = n; }
+    cnt++;
+    return;
+  }
+  int n2 = n / 2;
+  n2 -= n2 % 8;
+  pw_leaves<(L > 0 ? L - 1 : 0)>(off, n2, cnt, lane, my_off, my_n);
+  pw_leaves<(L > 0 ? L - 1 : 0)>(off + n2, n - n2, cnt, lane, my_off, my_n);
+}
+template <int L> __device__ inline double pw_combine(int n, int& cnt, double leaf) {
+  if (L == 0 || n <= 128) return __shfl(leaf, cnt++);
+  int n2 = n / 2;
+  n2 -= n2 % 8;
+  const double l = pw_combine<(L > 0 ? L - 1 : 0)>(n2, cnt, leaf);
+  return l + pw_combine<(L > 0 ? L - 1 : 0)>(n - n2, cnt, leaf);
+}
+// n <= 64 * 128 (callers here: a field's sync peaks, <= MAX_PEAKS)
+__device__ inline double wave_pw_sum(const double* a, int n, int lane) {
+  int cnt = 0, off = 0, m = 0;
+  pw_leaves<6>(0, n, cnt, lane, off, m);
+  const double leaf = (lane < cnt) ? pw_block(a + off, m) : 0.0;
+  cnt = 0;
+  return 0.0 + pw_combine<6>(n, cnt, leaf);
+}
+// np_std on one wave (tmp: n doubles of scratch, in LDS), result in every lane.
+__device__ inline double wave_np_std(const double* a, int n, double* tmp, int lane) {
+  const double m = wave_pw_sum(a, n, lane) / (double)n;
+  for (int i = lane; i < n; i += 64) { const double d = a[i] - m; tmp[i] = d * d; }
+  __syncthreads();
+  return sqrt(wave_pw_sum(tmp, n, lane) / (double)n);
+}
+
 __device__ inline bool inrange(double a, double lo, double hi) { return (a >= lo) && (a <= hi); }
 
 // np.round / Python round on doubles: half to even.
