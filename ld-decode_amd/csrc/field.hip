@@ -173,7 +173,8 @@ extern "C" __global__ __launch_bounds__(64) void ldg_k_sync(
     const int32_t* __restrict__ smap, const ReadDesc* __restrict__ reads, const double* __restrict__ video, int64_t vread_stride,
     int64_t vchan_stride, SysConst C, FieldRec* __restrict__ recs, int32_t* __restrict__ peaks,
     const int32_t* __restrict__ status, const int32_t* __restrict__ node_pos, const int32_t* __restrict__ node_pk,
-    const double* __restrict__ node_lv, const int32_t* __restrict__ node_n, const SyncTile* __restrict__ stiles) {
+    const double* __restrict__ node_lv, const int32_t* __restrict__ node_n, const SyncTile* __restrict__ stiles,
+    int nofast) {
   prio_latency();
 
   __shared__ int32_t s_npos[SEG_K * SEG_NMAX];
@@ -228,14 +229,91 @@ extern "C" __global__ __launch_bounds__(64) void ldg_k_sync(
       np += tot;
     }
   };
-  if (G.stop > 0) {
+  // per chain (lane k): the first node j* of chain k that chain k+1 also visits,
+  // and its index jn* there -- a merge of the two sorted position lists from the
+  // first position of chain k+1, all chains at once.  From j* on the two chains
+  // coincide (next() is a function of the position), so the stitch below needs
+  // no search when it enters chain k at or before j*, and one check otherwise.
+  static_assert(SEG_K == 64, "one lane per chain");
+  int jstar = -1, jnstar = -1;
+  if (G.stop > 0 && lane + 1 < SEG_K) {
+    const int c0 = s_cnt[lane], c1 = s_cnt[lane + 1];
+    if (c0 > 0 && c1 > 0) {
+      const int32_t* P = s_npos + lane * SEG_NMAX;
+      const int32_t* Q = s_npos + (lane + 1) * SEG_NMAX;
+      const int32_t q0 = Q[0];
+      int lo = 0, hi = c0;
+      while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (P[mid] < q0) lo = mid + 1; else hi = mid;
+      }
+      int i = lo, t = 0;
+      while (i < c0 && t < c1) {
+        const int32_t pi = P[i], qt = Q[t];
+        if (pi == qt) { jstar = i; jnstar = t; break; }
+        if (pi < qt) i++; else t++;
+      }
+    }
+  }
+  // Fast path: when every chain k < 63 is entered at or before its j* (the usual
+  // case), the path is chain k's nodes [a_k, j*_k) with a_0 = 0, a_k = jn*_{k-1},
+  // then chain 63 to its end; if that end's next position is past the walk's
+  // stop there is no direct-walk tail.  Then every chain's peaks go out at once
+  // (counts, a wave prefix sum, per-lane writes); otherwise the serial stitch.
+  bool done = false;
+  if (G.stop > 0 && !nofast) {
+    const int c0 = s_cnt[lane];
+    const int prev_jn = __shfl(jnstar, lane > 0 ? lane - 1 : 0);   // all lanes active for the shuffle
+    const int ak = (lane == 0) ? 0 : prev_jn;
+    int bk = c0;
+    bool ok = c0 > 0;
+    if (lane + 1 < SEG_K) {
+      ok = ok && s_cnt[lane + 1] > 0 && jstar >= 0 && ak <= jstar;
+      bk = jstar;
+    } else {
+      const int L = lane * SEG_NMAX + c0 - 1;
+      const int64_t pn = (c0 > 0) ? (s_npk[L] >= 0 ? (int64_t)s_npk[L] + G.jump : (int64_t)s_npos[L] + G.win) : 0;
+      ok = ok && ak <= c0 && pn >= G.stop;
+    }
+    if (__ballot(ok) == ~0ull) {
+      int c = 0;
+      for (int j = ak; j < bk; j++) c += s_npk[lane * SEG_NMAX + j] >= 0;
+      int incl = c;
+      for (int d = 1; d < 64; d <<= 1) {
+        const int v = __shfl_up(incl, d);
+        if (lane >= d) incl += v;
+      }
+      const int total = __shfl(incl, 63);
+      if (total <= MAX_PEAKS) {
+        int w = incl - c;
+        for (int j = ak; j < bk; j++) {
+          const int32_t pk = s_npk[lane * SEG_NMAX + j];
+          if (pk >= 0) { s_pk[w] = pk; s_lvi[w] = lane * SEG_NMAX + j; w++; }
+        }
+        np = total;
+        done = true;
+      }
+    }
+  }
+  if (G.stop > 0 && !done) {
     int k = 0, a = 0;
     while (!overflow) {
       const int cnt = s_cnt[k];
       const int32_t* pos = s_npos + k * SEG_NMAX;
       // b: first node j >= a of chain k that chain k+1 also visits
       int b = -1, jn = -1;
+      bool search = false;
       if (k + 1 < SEG_K && s_cnt[k + 1] > 0) {
+        const int js = __shfl(jstar, k), jns = __shfl(jnstar, k);
+        if (js >= a) {
+          b = js; jn = jns;
+        } else if (js >= 0 && a < cnt) {
+          const int t = jns + (a - js);
+          if (t < s_cnt[k + 1] && s_npos[(k + 1) * SEG_NMAX + t] == pos[a]) { b = a; jn = t; }
+          else search = true;                // not expected: fall back to the search
+        }
+      }
+      if (search) {
         const int32_t* pn = s_npos + (k + 1) * SEG_NMAX;
         for (int j0 = a; j0 < cnt && b < 0; j0 += 64) {
           const int j = j0 + lane;
