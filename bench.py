@@ -71,6 +71,11 @@ def cpu_baseline(seconds):
             'fields_per_s': 2 * len(frames) / dt}
 
 
+def progress(rank, what):
+    """a heartbeat on stderr (the JSON line stays the only stdout output)"""
+    print('[bench rank %d] %s' % (rank, what), file=sys.stderr, flush=True)
+
+
 def main():
     args = parse()
     world = int(os.environ.get('WORLD_SIZE', '1'))
@@ -97,13 +102,15 @@ def main():
     dec.ctx.synth(nsamp, fmt=args.fmt, first_frame=1 + 2000 * (rank % 39), seed=20181015 + rank)
     dec.use_resident_capture(args.fmt, nsamp)
     synth_s = time.perf_counter() - t0
+    progress(rank, 'capture synthesised (%.1f s)' % synth_s)
 
     def step():
         dec.use_resident_capture(args.fmt, nsamp)      # fresh read cache: no reuse across steps
         return dec.decode(sink=None, comb=not args.no_comb)
 
-    for _ in range(args.warmup):
+    for w in range(args.warmup):
         nfr = step()
+        progress(rank, 'warm-up step %d done' % (w + 1))
 
     def barrier():
         if dist is not None:
@@ -117,9 +124,10 @@ def main():
     t0 = time.perf_counter()
     frames = 0
     consumed = 0
-    for _ in range(args.steps):
+    for k in range(args.steps):
         frames += step()
         consumed += dec.last_meta['nextsample']
+        progress(rank, 'step %d done' % (k + 1))
     barrier()
     dt = time.perf_counter() - t0
     stats = dec.ctx.profile_stats()
