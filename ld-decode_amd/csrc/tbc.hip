@@ -628,11 +628,6 @@ extern "C" __global__ __launch_bounds__(FINAL_NT) void ldg_k_final_lines(
 }
 
 // Mark reads still pending after the whole chain as valid.
-extern "C" __global__ void ldg_k_finish(const int32_t* __restrict__ smap, FieldRec* __restrict__ recs, int n) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n && recs[smap[i]].status == FS_PENDING) recs[smap[i]].status = FS_VALID;
-}
-
 // ---------------------------------------------------------------------------
 // downscale_audio (lddecode_core.py:431-484) for n fields.  grid: n x 256.
 // Field i's inputs live at entry idx[i] of (recs, lines + entry * lines_stride,
