@@ -23,6 +23,8 @@
  *     lddecode_core.py:1238-1252
  *   comb-ntsc stdin/stdout frame stream, dim=2          ldg_comb_ntsc
  *     comb-ntsc.cxx:834-892, 1099-1117
+ *   PAL Y/C (build-defined adaptation of                 ldg_comb_pal
+ *     attic2/comb-pal.cxx:234-654, 820-917)
  *   cx-expander stdin/stdout (.pcm post-chain)          ldg_cx_process
  *     cx-expander.cxx:34-117
  *   comb-ntsc -d 3 -F [-c core] [-r range] (3D, no      ldg_comb_ntsc3d
@@ -215,6 +217,13 @@ int ldg_comb_ntsc_async(ldg_ctx* ctx, int n);
  * 3D); ldg_comb_reset also drops the held frames. */
 int ldg_comb_ntsc3d(ldg_ctx* ctx, int n, const uint16_t* frames, uint16_t* rgb_out, int* n_out, double core_ire,
                     double range_ire);
+/* PAL Y/C decoder (SURVEY §8 f, row F2), BUILD-DEFINED: the snapshot has no
+ * PAL comb for the 1135x625 .tbc geometry; this is attic2/comb-pal.cxx's dim=2
+ * path (Split1D / Split2D over lines +-4 / SplitIQ / AdjustY / Y-NR / burst
+ * angle rotation / V-switch flip / YUV->RGB) adapted to it (oracle/combpal.cpp
+ * states the choices).  n host frames of 1135x625 uint16 in, n rgb48 frames of
+ * 1057x576 out; the burst-level EMA carries across calls (ldg_comb_reset). */
+int ldg_comb_pal(ldg_ctx* ctx, int n, const uint16_t* frames, uint16_t* rgb_out);
 int ldg_sync(ldg_ctx* ctx);
 
 /* ---- in-library kernel timing (HIP events on the context's stream) ------------- */

@@ -70,8 +70,10 @@ __constant__ NRTaps g_nr = {{
 
 __device__ __forceinline__ double clampd(double v, double lo, double hi) { return v < lo ? lo : (v > hi ? hi : v); }
 
-// clp1 with the three clp0 rows staged in LDS (p = l-2, c = l, n = l+2).
-__device__ __forceinline__ double clp1_lds(const double* p1, const double* c1, const double* n1, int h) {
+// clp1 with the three clp0 rows staged in LDS (p = l-2, c = l, n = l+2; the
+// PAL decoder passes l-4 / l+4 and its own p_2drange = 45 * its irescale).
+__device__ __forceinline__ double clp1_lds(const double* p1, const double* c1, const double* n1, int h,
+                                           double p2drange = P_2DRANGE) {
   const double c0 = c1[h], cm = c1[h - 1];
   const double p0 = p1[h], pm = p1[h - 1];
   const double n0 = n1[h], nm = n1[h - 1];
@@ -83,8 +85,8 @@ __device__ __forceinline__ double clp1_lds(const double* p1, const double* c1, c
   kn -= (fabs(c0) + fabs(nm)) * .10;
   kp /= 2;
   kn /= 2;
-  kp = clampd(1 - (kp / P_2DRANGE), 0, 1);
-  kn = clampd(1 - (kn / P_2DRANGE), 0, 1);
+  kp = clampd(1 - (kp / p2drange), 0, 1);
+  kn = clampd(1 - (kn / p2drange), 0, 1);
   double sc = 1.0;
   if (kn != 0 || kp != 0) {
     if (kn > (3 * kp)) kp = 0;

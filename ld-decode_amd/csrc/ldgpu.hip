@@ -3,6 +3,7 @@
 #include "field.hip"
 #include "tbc.hip"
 #include "comb.hip"
+#include "combpal.hip"
 #include "synth.hip"
 #include "abi.inc"
 #include "cx.inc"

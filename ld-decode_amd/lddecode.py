@@ -42,7 +42,9 @@ def parse(argv=None):
     # MI355X additions
     p.add_argument('--device', type=int, default=0, help='HIP device')
     p.add_argument('--batch', type=int, default=96, help='field reads per GPU launch')
-    p.add_argument('--comb', action='store_true', help='also write <outfile>.rgb through the 2D NTSC comb')
+    p.add_argument('--comb', action='store_true',
+                   help='also write <outfile>.rgb through the 2D NTSC comb (PAL: the build-defined PAL Y/C '
+                        'decoder, 1057x576 rgb48)')
     p.add_argument('--comb-3d', action='store_true',
                    help='with --comb: the 3D comb without optical flow (comb-ntsc -d 3 -F); '
                         'every frame but the first and the last')
@@ -61,8 +63,8 @@ def main(argv=None):
         print("ERROR: Can only be PAL or NTSC")
         return 1
     system = 'PAL' if args.pal else 'NTSC'
-    if args.comb and system != 'NTSC':
-        print("ERROR: --comb is NTSC only")
+    if args.comb and system != 'NTSC' and args.comb_3d:
+        print("ERROR: --comb-3d is NTSC only")
         return 1
 
     world = int(os.environ.get('WORLD_SIZE', '1'))

@@ -600,8 +600,8 @@ class GPUDecoder:
         time offset is known only after the exchange), see self.shard_frames.
         Returns the number of frames decoded."""
         self.comb, self.comb_sink, self.comb3d = comb, comb_sink, (comb3d if comb else None)
-        if self.comb3d is not None and sink is None:
-            raise ValueError('the 3D comb runs on host frames (a sink is required)')
+        if (self.comb3d is not None or (comb and self.sysp.name == 'PAL')) and sink is None:
+            raise ValueError('the 3D and PAL combs run on host frames (a sink is required)')
         self.archive, self.arch_next, self.shard_frames = archive, 0, []
         self.transitions = []
         if comb:
@@ -714,7 +714,12 @@ class GPUDecoder:
         else:
             pics = self.ctx.assemble_frames(tops, bots, W, H)
             if self.comb:
-                rgb = self.ctx.comb_ntsc(pics) if self.comb3d is None else self.ctx.comb_ntsc3d(pics, *self.comb3d)
+                if self.sysp.name == 'PAL':
+                    rgb = self.ctx.comb_pal(pics)             # build-defined PAL Y/C (row F2)
+                elif self.comb3d is None:
+                    rgb = self.ctx.comb_ntsc(pics)
+                else:
+                    rgb = self.ctx.comb_ntsc3d(pics, *self.comb3d)
                 if self.comb_sink:
                     for r in rgb:
                         self.comb_sink(r)

@@ -22,7 +22,7 @@ EXPORTS = ['ldg_create', 'ldg_destroy', 'ldg_last_error', 'ldg_set_filters', 'ld
            'ldg_comb_ntsc', 'ldg_comb_reset', 'ldg_version', 'ldg_device_count', 'ldg_profile_enable',
            'ldg_profile_read', 'ldg_synth_capture', 'ldg_capture_download', 'ldg_comb_ntsc_async', 'ldg_sync',
            'ldg_archive_fields', 'ldg_archive_audio', 'ldg_decode_reads_async', 'ldg_decode_reads_wait',
-           'ldg_field_audio_async', 'ldg_field_audio_collect', 'ldg_comb_ntsc3d', 'ldg_cx_create', 'ldg_cx_destroy', 'ldg_cx_process']
+           'ldg_field_audio_async', 'ldg_field_audio_collect', 'ldg_comb_ntsc3d', 'ldg_cx_create', 'ldg_cx_destroy', 'ldg_cx_process', 'ldg_comb_pal']
 
 
 class FieldInfo(C.Structure):
@@ -112,6 +112,7 @@ def load(path=None):
                                       C.POINTER(C.c_uint32), C.c_int64]
     lib.ldg_capture_download.argtypes = [vp, vp, C.c_int64, C.c_int64]
     lib.ldg_capture_download.restype = C.c_int64
+    lib.ldg_comb_pal.argtypes = [vp, C.c_int, vp, vp]
     lib.ldg_cx_create.argtypes = [C.POINTER(vp)]
     lib.ldg_cx_destroy.argtypes = [vp]
     lib.ldg_cx_process.argtypes = [vp, C.c_int64, vp, vp]
@@ -313,6 +314,15 @@ class Context:
                                              out.ctypes.data_as(C.c_void_p), C.byref(n_out), core_ire, range_ire),
                     'ldg_comb_ntsc3d')
         return out[:n_out.value]
+
+    def comb_pal(self, frames):
+        """PAL Y/C decoder (build-defined, see include/ldgpu.h): n x (625, 1135) uint16 frames ->
+        n x (576, 1057, 3) rgb48."""
+        f = np.ascontiguousarray(frames, dtype=np.uint16).reshape(-1, 625 * 1135)
+        out = np.zeros((f.shape[0], 576, 1057, 3), dtype=np.uint16)
+        self._check(self.lib.ldg_comb_pal(self.h, f.shape[0], f.ctypes.data_as(C.c_void_p),
+                                          out.ctypes.data_as(C.c_void_p)), 'ldg_comb_pal')
+        return out
 
     def comb_ntsc_device(self, n):
         """Comb the first n frames of the context's device frame buffer (ldg_assemble_frames

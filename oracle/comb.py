@@ -77,3 +77,37 @@ class Comb3D:
     @property
     def aburstlev(self):
         return self.lib.comb3d_aburstlev(self.h)
+
+
+PAL_IN_X, PAL_IN_Y, PAL_OUT_W, PAL_OUT_H = 1135, 625, 1057, 576
+LIB_PAL = os.path.join(HERE, '_build', 'libcombpal.so')
+
+
+class CombPAL:
+    """The build-defined PAL Y/C decoder's checker (oracle/combpal.cpp): one process."""
+
+    def __init__(self):
+        if not os.path.exists(LIB_PAL) or os.path.getmtime(LIB_PAL) < os.path.getmtime(os.path.join(HERE, 'combpal.cpp')):
+            subprocess.check_call(['make', '-s', '-C', HERE])
+        self.lib = C.CDLL(LIB_PAL)
+        self.lib.combpal_create.restype = C.c_void_p
+        self.lib.combpal_destroy.argtypes = [C.c_void_p]
+        self.lib.combpal_process.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p]
+        self.lib.combpal_aburstlev.argtypes = [C.c_void_p]
+        self.lib.combpal_aburstlev.restype = C.c_double
+        self.h = self.lib.combpal_create()
+
+    def __del__(self):
+        if getattr(self, 'h', None):
+            self.lib.combpal_destroy(self.h)
+            self.h = None
+
+    def process(self, frames):
+        f = np.ascontiguousarray(frames, dtype=np.uint16).reshape(-1, PAL_IN_Y, PAL_IN_X)
+        out = np.zeros((f.shape[0], PAL_OUT_H, PAL_OUT_W, 3), dtype=np.uint16)
+        self.lib.combpal_process(self.h, f.shape[0], f.ctypes.data, out.ctypes.data)
+        return out
+
+    @property
+    def aburstlev(self):
+        return self.lib.combpal_aburstlev(self.h)

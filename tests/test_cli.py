@@ -165,3 +165,19 @@ def test_cli_comb_3d(tmp_path):
     from oracle.comb import Comb3D
     o = Comb3D().process(frames)
     assert np.abs(o.astype(np.int64) - rgb.astype(np.int64)).max() <= 1
+
+
+@pytest.mark.gpu
+def test_cli_pal_comb(tmp_path):
+    """lddecode.py -p --comb: PAL .tbc through the build-defined PAL Y/C decoder, against
+    its oracle on the same frames (+-1 LSB)."""
+    cap, gold = _golden_capture(tmp_path, case='pal_clv_u8_0p2s')
+    out = tmp_path / 'out'
+    r = run_cli('-p', '--comb', cap, out)
+    assert r.returncode == 0, r.stderr[-2000:]
+    frames = np.fromfile(str(out) + '.tbc', dtype=np.uint16).reshape(-1, 625, 1135)
+    rgb = np.fromfile(str(out) + '.rgb', dtype=np.uint16).reshape(-1, 576, 1057, 3)
+    assert len(frames) >= 1 and len(rgb) == len(frames)
+    from oracle.comb import CombPAL
+    o = CombPAL().process(frames)
+    assert np.abs(o.astype(np.int64) - rgb.astype(np.int64)).max() <= 1
