@@ -201,6 +201,10 @@ int64_t ldg_debug_read(ldg_ctx* ctx, int slot, int what, void* dst, int64_t cap)
  * NULL keeps the result in the context. */
 int ldg_comb_ntsc(ldg_ctx* ctx, int n, const uint16_t* frames, uint16_t* rgb_out, int io_is_device);
 int ldg_comb_reset(ldg_ctx* ctx);
+/* Start the comb from a given burst-level EMA (comb-ntsc.cxx:560-566; -1 = not
+ * yet initialised, as after ldg_comb_reset): a field-group shard's comb starts
+ * from the state the previous shard's frames end in (ldgpu/shard.py). */
+int ldg_comb_set_state(ldg_ctx* ctx, double aburstlev);
 /* Asynchronous form for a fused pipeline: comb the first n frames of the
  * context's frame buffer into its rgb buffer on a second stream, overlapped
  * with the next ldg_decode_reads; the next ldg_assemble_frames into the

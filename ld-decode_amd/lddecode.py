@@ -83,8 +83,8 @@ def main(argv=None):
             torch.cuda.set_device(local)
         dist.init_process_group('cpu:gloo,cuda:nccl' if rccl else 'gloo')
         args.device = local % max(1, ndev)
-        if args.comb:
-            print("ERROR: --comb is single-GPU in this build")
+        if args.comb and (system != 'NTSC' or args.comb_3d):
+            print("ERROR: a sharded decode runs the 2D NTSC comb only")
             return 1
     dec = GPUDecoder(system=system, device=args.device, batch=args.batch)
     samples_per_frame = dec.rf.samples_per_frame                 # int(fs / FPS) + 1
@@ -204,8 +204,9 @@ def sharded(args, dec, outname, firstframe, num_frames, nextsample, req_frames, 
     frame_bytes = dec.sysp.outlinelen * dec.sysp.frame_lines * 2
     first = sum(n for n, _ in sizes[:rank])
     pcm_off = sum(b for _, b in sizes[:rank])
+    exts = ('.tbc', '.pcm', '.rgb') if args.comb else ('.tbc', '.pcm')
     if rank == 0:
-        for ext in ('.tbc', '.pcm'):
+        for ext in exts:
             open(outname + ext, 'wb').close()
     dist.barrier()
     with open(outname + '.tbc', 'r+b') as tbc, open(outname + '.pcm', 'r+b') as pcm:
@@ -215,6 +216,18 @@ def sharded(args, dec, outname, firstframe, num_frames, nextsample, req_frames, 
             print('frame ', meta['vbi']['framenr'])
             tbc.write(pic.tobytes())
             pcm.write(audio.tobytes())
+    if args.comb:
+        # the comb's burst-level EMA chains through every frame in order: each shard
+        # starts from the state the earlier shards' frames end in (exact, on the host)
+        from ldgpu.shard import comb_burst_levels, comb_start_state
+        pics = [pic for _, pic, _, _ in res]
+        levels = allgather(comb_burst_levels(pics))
+        dec.ctx.comb_set_state(comb_start_state(levels, rank))
+        rgb_bytes = 744 * 480 * 3 * 2
+        with open(outname + '.rgb', 'r+b') as fh:
+            fh.seek(first * rgb_bytes)
+            for i in range(0, len(pics), dec.ctx.max_frames):
+                fh.write(dec.ctx.comb_ntsc(np.stack(pics[i:i + dec.ctx.max_frames])).tobytes())
     metas = allgather([m for _, _, _, m in res])
     total = sum(n for n, _ in sizes)
     if rank == 0:

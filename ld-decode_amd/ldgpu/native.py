@@ -22,7 +22,7 @@ EXPORTS = ['ldg_create', 'ldg_destroy', 'ldg_last_error', 'ldg_set_filters', 'ld
            'ldg_comb_ntsc', 'ldg_comb_reset', 'ldg_version', 'ldg_device_count', 'ldg_profile_enable',
            'ldg_profile_read', 'ldg_synth_capture', 'ldg_capture_download', 'ldg_comb_ntsc_async', 'ldg_sync',
            'ldg_archive_fields', 'ldg_archive_audio', 'ldg_decode_reads_async', 'ldg_decode_reads_wait',
-           'ldg_field_audio_async', 'ldg_field_audio_collect', 'ldg_comb_ntsc3d', 'ldg_cx_create', 'ldg_cx_destroy', 'ldg_cx_process', 'ldg_comb_pal']
+           'ldg_field_audio_async', 'ldg_field_audio_collect', 'ldg_comb_ntsc3d', 'ldg_cx_create', 'ldg_cx_destroy', 'ldg_cx_process', 'ldg_comb_pal', 'ldg_comb_set_state']
 
 
 class FieldInfo(C.Structure):
@@ -113,6 +113,7 @@ def load(path=None):
     lib.ldg_capture_download.argtypes = [vp, vp, C.c_int64, C.c_int64]
     lib.ldg_capture_download.restype = C.c_int64
     lib.ldg_comb_pal.argtypes = [vp, C.c_int, vp, vp]
+    lib.ldg_comb_set_state.argtypes = [vp, C.c_double]
     lib.ldg_cx_create.argtypes = [C.POINTER(vp)]
     lib.ldg_cx_destroy.argtypes = [vp]
     lib.ldg_cx_process.argtypes = [vp, C.c_int64, vp, vp]
@@ -335,6 +336,9 @@ class Context:
 
     def sync(self):
         self._check(self.lib.ldg_sync(self.h), 'ldg_sync')
+
+    def comb_set_state(self, aburstlev):
+        self._check(self.lib.ldg_comb_set_state(self.h, float(aburstlev)), 'ldg_comb_set_state')
 
     def comb_reset(self):
         self._check(self.lib.ldg_comb_reset(self.h), 'ldg_comb_reset')

@@ -282,3 +282,35 @@ def decode_sharded(dec, rank, world, allgather, sink=None, start_frame=0, length
         raise RuntimeError('sharded decode: chain did not converge')
     res = sd.finish(summ)
     return [(g, pic, a, m) for (g, a, m), pic in zip(res, sd.frames)]
+
+
+# ---- the comb's chained state across shards -------------------------------------
+COMB_LINE0, COMB_LINES, NTSC_IRESCALE = 38, 525 - 38, 358.4
+
+
+def comb_burst_levels(frames):
+    """The burst levels ToRGB reads (comb-ntsc.cxx:560-561: raw[l * 910 + 1] / irescale,
+    lines 38..524), in frame order, for a list of 525x910 .tbc frames."""
+    if not len(frames):
+        return np.zeros(0)
+    f = np.asarray(frames, dtype=np.uint16).reshape(-1, 525, 910)
+    return (f[:, COMB_LINE0:525, 1].astype(np.float64) / NTSC_IRESCALE).reshape(-1)
+
+
+def comb_chain(a, levels):
+    """The aburstlev EMA (comb-ntsc.cxx:562-565) run over `levels` from state a, in
+    the kernel's and the reference's arithmetic order (exact)."""
+    for b in levels.tolist():
+        if b > 3:
+            if a < 0:
+                a = b
+            a = (a * .99) + (b * .01)
+    return a
+
+
+def comb_start_state(levels_by_rank, rank):
+    """The EMA a shard's comb starts from: the chain over every earlier shard's frames."""
+    a = -1.0
+    for r in range(rank):
+        a = comb_chain(a, levels_by_rank[r])
+    return a

@@ -104,23 +104,24 @@ def test_cli_seek_and_cut(tmp_path):
 @pytest.mark.gpu
 def test_cli_sharded_two_ranks_equal_single(tmp_path):
     """torch.distributed.run with 2 ranks (field-group sharding) writes the same
-    .tbc / .pcm / .json as the single-process CLI."""
+    .tbc / .pcm / .json, and with --comb the same .rgb (the comb's burst-level EMA
+    handed across the shard boundary), as the single-process CLI."""
     import socket
     from ldgpu.synth import make_capture
     data = make_capture(int(40e6 * 0.6), 'u8', first_frame=500, seed=13)
     cap = tmp_path / 'cap.u8'
     cap.write_bytes(bytes(data))
-    r = run_cli(cap, tmp_path / 'one')
+    r = run_cli('--comb', cap, tmp_path / 'one')
     assert r.returncode == 0, r.stderr[-2000:]
     with socket.socket() as sk:
         sk.bind(('127.0.0.1', 0))
         port = sk.getsockname()[1]
     env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY='0')
     r = subprocess.run([sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', '--nproc-per-node', '2',
-                        '--master-addr', '127.0.0.1', '--master-port', str(port), CLI, str(cap),
+                        '--master-addr', '127.0.0.1', '--master-port', str(port), CLI, '--comb', str(cap),
                         str(tmp_path / 'two')], capture_output=True, text=True, timeout=600, env=env)
     assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-3000:])
-    for ext in ('.tbc', '.pcm'):
+    for ext in ('.tbc', '.pcm', '.rgb'):
         assert (tmp_path / ('one' + ext)).read_bytes() == (tmp_path / ('two' + ext)).read_bytes(), ext
     assert json.load(open(tmp_path / 'one.json')) == json.load(open(tmp_path / 'two.json'))
 

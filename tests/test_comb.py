@@ -250,3 +250,18 @@ def test_gpu_comb3d_on_decoded_frames():
     o = Comb3D().process(fr)
     assert g.shape[0] == fr.shape[0] - 2
     assert np.abs(g.astype(np.int64) - o.astype(np.int64)).max() <= 1
+
+
+@pytest.mark.gpu
+def test_gpu_comb_set_state_continues_the_chain(gpu_ctx_ntsc):
+    """ldg_comb_set_state with the host chain's state over the first frames makes the
+    comb of the rest equal to the uninterrupted run (the sharded --comb handover)."""
+    from ldgpu.shard import comb_burst_levels, comb_chain
+    ctx, _ = gpu_ctx_ntsc
+    fr = frames_3d(seed=12, n=5)
+    ctx.comb_reset()
+    full = ctx.comb_ntsc(fr)
+    ctx.comb_set_state(comb_chain(-1.0, comb_burst_levels(fr[:2])))
+    part = ctx.comb_ntsc(fr[2:])
+    assert np.array_equal(full[2:], part)
+    ctx.comb_reset()

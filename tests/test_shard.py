@@ -211,3 +211,16 @@ def test_sharded_window_miss_falls_back_to_whole_capture():
     assert len(got) == len(want)
     for (gf, ga, gm), (wf, wa, wm) in zip(got, want):
         assert gm == wm and np.array_equal(gf, wf) and np.array_equal(ga, wa)
+
+
+def test_comb_start_state_matches_one_chain():
+    """The comb state a shard starts from is the single chain's state at that frame."""
+    from ldgpu.shard import comb_burst_levels, comb_chain, comb_start_state
+    rng = np.random.default_rng(6)
+    frames = rng.integers(0, 65535, (5, 525, 910)).astype(np.uint16)
+    frames[:, :, 1] = rng.integers(0, 20 * 358, (5, 525))          # burst levels 0..20 IRE
+    frames[0, :100, 1] = 0                                         # the chain starts late
+    lv = [comb_burst_levels(frames[:2]), comb_burst_levels(frames[2:3]), comb_burst_levels(frames[3:])]
+    whole = comb_chain(-1.0, comb_burst_levels(frames[:3]))
+    assert comb_start_state(lv, 2) == whole
+    assert comb_start_state(lv, 0) == -1.0
