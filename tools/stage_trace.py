@@ -10,7 +10,7 @@ sys.path.insert(0, os.path.join(ROOT, 'ld-decode_amd'))
 def main():
     from ldgpu import native
     from ldgpu.rfparams import RFTables
-    batch, reps = 64, int(os.environ.get('REPS', '12'))
+    batch, reps = int(os.environ.get('BATCH', '64')), int(os.environ.get('REPS', '12'))
     depth = int(os.environ.get('LDG_DEPTH', '2'))
     rf = RFTables('NTSC')
     ctx = native.Context('NTSC', 0, max_reads=depth * batch)
