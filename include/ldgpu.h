@@ -242,6 +242,10 @@ typedef struct ldg_kernel_stat {
 int ldg_profile_enable(ldg_ctx* ctx, int on);
 /* Copy up to max per-kernel records; returns the number of kernels recorded. */
 int ldg_profile_read(ldg_ctx* ctx, ldg_kernel_stat* out, int max);
+/* The demod launches' execution spans since ldg_profile_enable (first workgroup
+ * start to last workgroup end on the device's constant-rate clock, what a
+ * kernel trace reports): count and summed milliseconds. */
+int ldg_profile_spans(ldg_ctx* ctx, double* total_ms, int64_t* count);
 
 /* ---- benchmark / test tooling (not a reference interface) ----------------------
  * Synthesise an NTSC LaserDisc RF capture directly into this context's HBM

@@ -196,11 +196,15 @@ extern "C" __global__ __launch_bounds__(1024) void ldg_k_demod(
     const double2* __restrict__ a_lfilt, const double2* __restrict__ a_rfilt, SysConst C,
     double* __restrict__ video, int64_t vread_stride, int64_t vchan_stride,
     double* __restrict__ audio1, int64_t aread_stride, int64_t achan_stride, int32_t* __restrict__ status,
-    double2* __restrict__ ospill, SyncTile* __restrict__ stiles, double2* __restrict__ aslice) {
+    double2* __restrict__ ospill, SyncTile* __restrict__ stiles, double2* __restrict__ aslice,
+    unsigned long long* __restrict__ span) {
   __shared__ double2 s_x[M];          // 128 KiB: the 8192-point transforms
   const CBuf X_{s_x};
   const int tid = threadIdx.x;
   STAMP(0);
+  // profiling: the launch's execution span on the constant-rate clock (first
+  // workgroup start, last workgroup end), what a kernel trace reports
+  if (span && tid == 0) atomicMax(&span[0], ~(unsigned long long)__builtin_amdgcn_s_memrealtime());
   const int slot = smap[blockIdx.x / MAX_BLOCKS_PER_READ];
   const int b = blockIdx.x % MAX_BLOCKS_PER_READ;
   const ReadDesc rd = reads[slot];
@@ -448,6 +452,7 @@ extern "C" __global__ __launch_bounds__(1024) void ldg_k_demod(
     }
     STAMP(14 + 3 * e);
   }
+  if (span && tid == 0) atomicMax(&span[1], (unsigned long long)__builtin_amdgcn_s_memrealtime());
 }
 
 // ---------------------------------------------------------------------------
