@@ -38,7 +38,9 @@ def main():
     print(json.dumps({'metric': 'RF Msamples/s (40 MSPS PAL CLV, RF->.tbc+.pcm)', 'value': round(msps, 1),
                       'fields_per_s': round(2 * frames / dt, 1), 'realtime_x': round(msps / 40.0, 1),
                       'frames_per_step': frames // steps, 'seconds_of_rf': secs, 'steps': steps,
-                      'synth_s': round(synth_s, 1), 'reads_decoded_total': dec.stats['reads']}))
+                      'synth_s': round(synth_s, 1), 'reads_decoded_total': dec.stats['reads'],
+                      'reads_used_total': dec.stats['reads_used'], 'batches': dec.stats['batches'],
+                      'misses': dec.stats.get('misses', 0), 'miss_sample': dec.stats.get('miss_log', [])[:8]}))
 
 
 if __name__ == '__main__':
