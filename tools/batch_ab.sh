@@ -2,7 +2,7 @@
 # A/B of the launch batch size, interleaved so that box-level drift hits both
 cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out
-for rep in 1 2; do
+for rep in ${REPS_AB:-1 2}; do
   for b in ${BATCHES:-64 96}; do
     timeout -k 10 200 python bench.py --no-cpu --batch $b --steps 3 > gpurun_out/ab_${b}_${rep}.log 2>&1 || exit 1
     python -c "
