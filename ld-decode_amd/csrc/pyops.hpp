@@ -311,12 +311,12 @@ __device__ inline double wave_kth(const double* a, int n, int k, int lane, int* 
       if (lane >= o) incl += v;
     }
     const int excl = incl - tot;
-    int digit = -1, below = 0;
+    int digit = -1, below = 0, cnt = 0;
     if (k >= excl && k < incl) {
       int run = excl;
 #pragma unroll
       for (int e = 0; e < 4; e++) {
-        if (digit < 0 && k < run + c[e]) { digit = 4 * lane + e; below = run; }
+        if (digit < 0 && k < run + c[e]) { digit = 4 * lane + e; below = run; cnt = c[e]; }
         run += c[e];
       }
     }
@@ -324,10 +324,23 @@ __device__ inline double wave_kth(const double* a, int n, int k, int lane, int* 
     const int src = __ffsll((unsigned long long)m) - 1;
     digit = __shfl(digit, src);
     below = __shfl(below, src);
+    cnt = __shfl(cnt, src);
     k -= below;
     prefix |= (uint64_t)digit << shift;
     mask |= (uint64_t)255 << shift;
     __syncthreads();
+    if (cnt == 1 && shift > 0) {
+      // one key left with this prefix: it is the k-th; fetch it instead of more passes
+      uint64_t key = 0;
+      bool hit = false;
+      for (int i = lane; i < n && !hit; i += 64) {
+        const uint64_t u = (uint64_t)__double_as_longlong(a[i]);
+        if ((u & mask) == prefix) { key = u; hit = true; }
+      }
+      const uint64_t hm = __ballot(hit);
+      const int hs = __ffsll((unsigned long long)hm) - 1;
+      return __longlong_as_double((long long)__shfl((long long)key, hs));
+    }
   }
   return __longlong_as_double((long long)prefix);
 }
@@ -383,12 +396,12 @@ __device__ inline uint64_t wave_kth_key(const double* a, int n, int k, int lane,
       if (lane >= o) incl += v;
     }
     const int excl = incl - tot;
-    int digit = -1, below = 0;
+    int digit = -1, below = 0, cnt = 0;
     if (k >= excl && k < incl) {
       int run = excl;
 #pragma unroll
       for (int e = 0; e < 4; e++) {
-        if (digit < 0 && k < run + c[e]) { digit = 4 * lane + e; below = run; }
+        if (digit < 0 && k < run + c[e]) { digit = 4 * lane + e; below = run; cnt = c[e]; }
         run += c[e];
       }
     }
@@ -396,10 +409,23 @@ __device__ inline uint64_t wave_kth_key(const double* a, int n, int k, int lane,
     const int src = __ffsll((unsigned long long)m) - 1;
     digit = __shfl(digit, src);
     below = __shfl(below, src);
+    cnt = __shfl(cnt, src);
     k -= below;
     prefix |= (uint64_t)digit << shift;
     mask |= (uint64_t)255 << shift;
     __syncthreads();
+    if (cnt == 1 && shift > 0) {
+      // one key left with this prefix: it is the k-th; fetch it instead of more passes
+      uint64_t key = 0;
+      bool hit = false;
+      for (int i = lane; i < n && !hit; i += 64) {
+        const uint64_t u = dkey(a[i]);
+        if ((u & mask) == prefix) { key = u; hit = true; }
+      }
+      const uint64_t hm = __ballot(hit);
+      const int hs = __ffsll((unsigned long long)hm) - 1;
+      return (uint64_t)__shfl((long long)key, hs);
+    }
   }
   return prefix;
 }
