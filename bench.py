@@ -11,6 +11,7 @@ with the .tbc frames assembled in HBM.  Ranks decode independent captures
 (fields shard by capture; no data-path collective).
 """
 import argparse
+import contextlib
 import json
 import os
 import sys
@@ -60,7 +61,9 @@ def cpu_baseline(seconds):
     from oracle.capture import FMT_U8
     from oracle.framer import decode_capture
     data = make_capture(int(40e6 * seconds), 'u8', seed=99)
-    with threadpool_limits(limits=1):
+    # the oracle prints the reference's log lines ('not valid', ...): to stderr, so
+    # the JSON line stays the only stdout output
+    with threadpool_limits(limits=1), contextlib.redirect_stdout(sys.stderr):
         t0 = time.perf_counter()
         frames, pcm, meta = decode_capture(data, FMT_U8)
         dt = time.perf_counter() - t0

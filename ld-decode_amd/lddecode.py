@@ -198,8 +198,11 @@ def sharded(args, dec, outname, firstframe, num_frames, nextsample, req_frames, 
         print('rank %d: a read left the capture window; using the whole capture' % rank)
         dec.set_capture(raw, fmt)
 
+    # the rank's frames wait in a spill file beside the outputs until their global
+    # offsets are known (bounded host memory for any capture length)
     res = decode_sharded(dec, rank, world, allgather, start_frame=firstframe, length=num_frames,
-                         start_sample=nextsample, whole_capture=whole)
+                         start_sample=nextsample, whole_capture=whole,
+                         spill_dir=os.path.dirname(os.path.abspath(outname)))
     sizes = allgather((len(res), sum(a.nbytes for _, _, a, _ in res)))
     frame_bytes = dec.sysp.outlinelen * dec.sysp.frame_lines * 2
     first = sum(n for n, _ in sizes[:rank])

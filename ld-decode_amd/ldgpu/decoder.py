@@ -144,7 +144,7 @@ class GPUField:
 
 
 class FrameOut:
-    __slots__ = ('top', 'bottom', 'audio_fields', 'vbi', 'nextsample', 'fields', 'index', 'start', 'tstart')
+    __slots__ = ('top', 'bottom', 'audio_fields', 'vbi', 'nextsample', 'fields', 'index', 'start', 'tstart', 'mtf0')
 
     def __init__(self, **kw):
         for k, v in kw.items():
@@ -682,6 +682,7 @@ class GPUDecoder:
                 nframes_read += 1
                 fr.start = nextsample
                 fr.tstart = cp[6]
+                fr.mtf0 = cp[1]                 # the MTF this frame's readframe began with (the chain state)
                 nextsample = fr.nextsample
                 if keep_from is not None and fr.start < keep_from:
                     continue                    # warm-up frame: chains only
@@ -733,7 +734,7 @@ class GPUDecoder:
                 self.shard_frames.append({'index': fr.index, 'start': int(fr.start), 'tstart': fr.tstart,
                                           'nextsample': int(fr.nextsample),
                                           'audio': ents, 'vbi': dict(fr.vbi), 'fields': fr.fields,
-                                          'mtf': float(fr.top.mtf_level)})
+                                          'mtf': float(fr.top.mtf_level), 'mtf0': float(fr.mtf0)})
             self.arch_next += len(af)
             af = []
         # the audio runs while the host plans and replays the next batch: this batch's

@@ -37,6 +37,8 @@ capture buffers when every rank has its own GPU, gloo through host memory
 otherwise.  A read that still falls outside the window raises WindowMiss and
 the rank re-runs with the whole capture.
 """
+import tempfile
+
 import numpy as np
 
 from .decoder import WindowMiss
@@ -137,7 +139,10 @@ def replay_offsets(o0, transitions, line_period):
 
 
 def check_chain(summaries):
-    """Ranks whose first frame does not continue the previous rank's chain (exactly)."""
+    """Ranks whose first frame does not continue the previous rank's chain (exactly).
+    first_mtf is the MTF in force when the first kept frame's readframe began (the
+    framer's checkpoint, before any MTF re-read inside it), which is what the
+    previous rank hands over as end_mtf."""
     bad = []
     prev = None
     for k, s in enumerate(summaries):
@@ -167,13 +172,68 @@ def frame_offsets(summaries):
     return out
 
 
+class FrameSpill:
+    """A rank's output frames on storage until the exchange has fixed their global
+    offsets: appended as they arrive, read back through a memory map.  Host memory
+    stays bounded by one frame, whatever the shard's length (an hour of NTSC is
+    ~13 GB of .tbc frames per rank on 8 GPUs)."""
+
+    def __init__(self, directory=None):
+        self.directory = directory
+        self.fh = None
+        self.shape = None
+        self.n = 0
+        self._map = None
+
+    def reset(self):
+        self.close()
+        self.fh = tempfile.TemporaryFile(prefix='ldgpu_shard_', dir=self.directory)
+        self.n = 0
+
+    def append(self, pic):
+        pic = np.ascontiguousarray(pic)
+        if self.shape is None:
+            self.shape, self.dtype = pic.shape, pic.dtype
+        assert pic.shape == self.shape and pic.dtype == self.dtype
+        self._map = None
+        self.fh.write(pic.tobytes())
+        self.n += 1
+
+    def _frames(self):
+        if self._map is None and self.n:
+            self.fh.flush()
+            self._map = np.memmap(self.fh, dtype=self.dtype, mode='r', shape=(self.n,) + tuple(self.shape))
+        return self._map
+
+    def __len__(self):
+        return self.n
+
+    def __getitem__(self, i):
+        if isinstance(i, slice):
+            m = self._frames()
+            return m[i] if m is not None else []
+        if not -self.n <= i < self.n:
+            raise IndexError(i)
+        return self._frames()[i]
+
+    def __iter__(self):
+        return (self[i] for i in range(self.n))
+
+    def close(self):
+        self._map = None
+        if self.fh is not None:
+            self.fh.close()
+            self.fh = None
+
+
 class ShardedDecode:
     """One rank's part of a field-group sharded decode, in two phases."""
 
     def __init__(self, dec, rank, world, start_frame=0, warmup_frames=2, length=None, start_sample=None,
-                 whole_capture=None):
+                 whole_capture=None, spill_dir=None):
         """whole_capture: callable that makes the whole capture resident (the fallback
-        when a capture window turns out too small)."""
+        when a capture window turns out too small).  spill_dir: where the output
+        frames wait for the exchange (FrameSpill; default: the system temp dir)."""
         self.dec, self.rank, self.world = dec, rank, world
         self.whole_capture, self.window_misses = whole_capture, 0
         self.spf = dec.rf.samples_per_frame
@@ -183,7 +243,7 @@ class ShardedDecode:
         self.start = start_frame * self.spf if start_sample is None else start_sample
         self.bounds = shard_bounds(self.start, dec.cap_nsamples, self.spf, world)
         self.warmup = warmup_frames
-        self.frames = []                    # (frame uint16 or None, local record)
+        self.frames = FrameSpill(spill_dir)   # this rank's output frames, in order
 
     def _run(self, sink, start_sample, keep_from, firstframe, init=None):
         dec = self.dec
@@ -195,7 +255,7 @@ class ShardedDecode:
                 sink(pic, None, meta)
 
         for attempt in range(2):
-            self.frames = []
+            self.frames.reset()
             try:
                 dec.decode(start_sample=start_sample, stop_sample=stop, keep_from=keep_from, firstframe=firstframe,
                            archive=True, sink=keep, init_state=init)
@@ -221,7 +281,7 @@ class ShardedDecode:
         t0 = sf[0]['tstart'] if sf else len(dec.transitions)
         return {'rank': self.rank, 'n': len(sf),
                 'first_start': sf[0]['start'] if sf else None,
-                'first_mtf': sf[0]['mtf'] if sf else None,
+                'first_mtf': sf[0]['mtf0'] if sf else None,
                 'last_next': sf[-1]['nextsample'] if sf else None,
                 'end_mtf': float(dec.mtf_level), 'end_framenr': dec.last_framenr, 'end_isclv': dec.last_isclv,
                 'transitions': list(dec.transitions[t0:]), 't0': t0}
@@ -265,12 +325,13 @@ class ShardedDecode:
 
 
 def decode_sharded(dec, rank, world, allgather, sink=None, start_frame=0, length=None, start_sample=None,
-                   whole_capture=None):
+                   whole_capture=None, spill_dir=None):
     """Run all phases with `allgather(obj) -> [obj per rank]` (torch.distributed
     all_gather_object, or an in-process stand-in).  Returns this rank's
-    [(global_index, frame, pcm, meta)]."""
+    [(global_index, frame, pcm, meta)]; the frames are memory-mapped views of the
+    rank's spill file (FrameSpill), valid while the returned list's frames are."""
     sd = ShardedDecode(dec, rank, world, start_frame, length=length, start_sample=start_sample,
-                       whole_capture=whole_capture)
+                       whole_capture=whole_capture, spill_dir=spill_dir)
     summ = allgather(sd.local())
     for _ in range(world):
         bad = check_chain(summ)
@@ -288,13 +349,18 @@ def decode_sharded(dec, rank, world, allgather, sink=None, start_frame=0, length
 COMB_LINE0, COMB_LINES, NTSC_IRESCALE = 38, 525 - 38, 358.4
 
 
-def comb_burst_levels(frames):
+def comb_burst_levels(frames, chunk=64):
     """The burst levels ToRGB reads (comb-ntsc.cxx:560-561: raw[l * 910 + 1] / irescale,
-    lines 38..524), in frame order, for a list of 525x910 .tbc frames."""
+    lines 38..524), in frame order, for a sequence of 525x910 .tbc frames (a list,
+    an array or a FrameSpill; read `chunk` frames at a time)."""
     if not len(frames):
         return np.zeros(0)
-    f = np.asarray(frames, dtype=np.uint16).reshape(-1, 525, 910)
-    return (f[:, COMB_LINE0:525, 1].astype(np.float64) / NTSC_IRESCALE).reshape(-1)
+    out = []
+    for i in range(0, len(frames), chunk):
+        part = frames[i:i + chunk]
+        f = np.asarray(part if not isinstance(part, list) else np.stack(part), dtype=np.uint16).reshape(-1, 525, 910)
+        out.append((f[:, COMB_LINE0:525, 1].astype(np.float64) / NTSC_IRESCALE).reshape(-1))
+    return np.concatenate(out)
 
 
 def comb_chain(a, levels):

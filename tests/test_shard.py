@@ -44,6 +44,50 @@ def test_offsets_equal_sequential_replay():
     assert check_chain(bad) == [1]
 
 
+class _FakeDec:
+    """The state ShardedDecode.summary reads from a GPUDecoder after a shard's decode."""
+
+    def __init__(self, frames, mtf_level):
+        self.shard_frames, self.mtf_level = frames, mtf_level
+        self.transitions, self.last_framenr, self.last_isclv = [262] * len(frames), 12000, False
+
+
+def test_chain_check_uses_the_mtf_before_a_reread():
+    """A CAV picture number >= 10000 clamps the MTF to 0 (lddecode_core.py:1300-1309).
+    The warm-up frames of shard 1 carry no picture number, so its first kept frame
+    begins with MTF 1 and re-reads itself at MTF 0, while the single decode (and
+    shard 0, whose end MTF is 0) reads it at MTF 0 once.  The frame's fields then
+    carry MTF 0 either way: the check must compare the MTF the frame's readframe
+    began with, and flag the shard."""
+    from ldgpu.shard import ShardedDecode
+    sd = ShardedDecode.__new__(ShardedDecode)
+    sd.rank = 1
+    sd.dec = _FakeDec([{'start': 5725434, 'tstart': 0, 'nextsample': 7060101, 'mtf': 0.0, 'mtf0': 1.0,
+                        'audio': [], 'vbi': {}, 'fields': []}], 0.0)
+    s1 = sd.summary()
+    s0 = {'rank': 0, 'n': 4, 'first_start': 385743, 'first_mtf': 0.0, 'last_next': 5725434, 'end_mtf': 0.0,
+          'transitions': [262] * 4, 't0': 0}
+    assert s1['first_mtf'] == 1.0 and check_chain([s0, s1]) == [1]
+    sd.dec.shard_frames[0]['mtf0'] = 0.0          # began at the handed-over MTF: no re-read, chain exact
+    assert check_chain([s0, sd.summary()]) == []
+
+
+def test_frame_spill_round_trip(tmp_path):
+    """A shard's frames wait on storage (bounded host memory) and read back unchanged."""
+    from ldgpu.shard import FrameSpill, comb_burst_levels
+    rng = np.random.default_rng(3)
+    frames = rng.integers(0, 65535, (5, 525, 910)).astype(np.uint16)
+    sp = FrameSpill(str(tmp_path))
+    sp.reset()
+    for f in frames:
+        sp.append(f)
+    assert len(sp) == 5 and np.array_equal(sp[3], frames[3]) and np.array_equal(np.stack(list(sp)), frames)
+    assert np.array_equal(comb_burst_levels(sp, chunk=2), comb_burst_levels(list(frames)))
+    sp.reset()                                    # a re-decode starts a fresh file
+    assert len(sp) == 0
+    sp.close()
+
+
 def test_shard_bounds_cover_the_capture():
     spf = 1334668
     b = shard_bounds(0, 2_400_000_000, spf, 8)
@@ -158,7 +202,8 @@ def test_sharded_decode_equals_single_decode(world, windowed):
     decs = [GPUDecoder(system='NTSC', batch=8) for _ in range(world)]
     raw = np.frombuffer(data, np.uint8)
     n = raw.size
-    w = shard_windows(shard_bounds(0, n, SPF - 1, world), SPF - 1, n)
+    spf = decs[0].rf.samples_per_frame          # the windows production computes (lddecode.load_window)
+    w = shard_windows(shard_bounds(0, n, spf, world), spf, n)
     sds = []
     for r, d in enumerate(decs):
         if windowed:
@@ -196,8 +241,9 @@ def test_sharded_window_miss_falls_back_to_whole_capture():
     ref.set_capture(data, 0)
     want = []
     ref.decode(sink=lambda fr, au, m: want.append((fr.copy(), au.copy(), m)))
-    w = shard_windows(shard_bounds(0, n, SPF - 1, 2), SPF - 1, n, halo_frames=0)
     decs = [GPUDecoder(system='NTSC', batch=8) for _ in range(2)]
+    spf = decs[0].rf.samples_per_frame
+    w = shard_windows(shard_bounds(0, n, spf, 2), spf, n, halo_frames=0)
     sds = []
     for r, d in enumerate(decs):
         lo, cut, _ = w[r]
