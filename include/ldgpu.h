@@ -117,11 +117,18 @@ typedef struct ldg_params {
  *   rfvideo[16384], mtf[16384], fvideo[16384], fvideo05[16384], fvideoburst[16384],
  *   fvideopilot[16384] (PAL; may be NULL for NTSC), fpsync[16384],
  *   audio_lfilt[1024], audio_rfilt[1024], audio_lpf2[4096];
+ * (fvideoburst, fvideopilot and fpsync are checked against `iir`, not used per sample)
  * real float64: mtf_logabs[16384] = log|MTF|, mtf_arg[16384] = arg MTF. */
 typedef struct ldg_filters {
   const double *rfvideo, *mtf, *fvideo, *fvideo05, *fvideoburst, *fvideopilot, *fpsync;
   const double *audio_lfilt, *audio_rfilt, *audio_lpf2;
   const double *mtf_logabs, *mtf_arg;
+  /* The butter(1) designs the tables sample (lddecode_core.py:204-214), 13 doubles:
+   * FPsync {b0, b1, a1}, Fburst {b0, b1, b2, a1, a2}, Fpilot {b0, b1, b2, a1, a2}
+   * (zeros for NTSC).  The demod filters sync, burst and pilot as these
+   * recurrences; ldg_set_filters checks fpsync = B/A and fvideoburst
+   * (fvideopilot) = fvideo * B/A on every bin and fails with LDG_EINVAL otherwise. */
+  const double *iir;
 } ldg_filters;
 
 int ldg_create(const ldg_config* cfg, ldg_ctx** out);

@@ -11,11 +11,13 @@
 // end (1 LSB of .tbc = 33.9 Hz).
 //
 // Per block, 8192-point FFTs: raw R2C, analytic even, analytic odd, demod R2C,
-// one C2R per output filter (video, burst, [pilot], 0.5 MHz), sync R2C, sync
-// C2R  = 9 (NTSC) / 10 (PAL); plus 2 x 1024-point audio IFFTs.
+// C2R 0.5 MHz, C2R video = 6 (NTSC and PAL).  The sync, burst and pilot
+// channels, whose filters are sampled butter(1) designs, are their periodic
+// recurrences in the time domain (iir.hpp).
 #include <hip/hip_runtime.h>
 #include "common.hpp"
 #include "fft8k.hpp"
+#include "iir.hpp"
 
 using namespace ldg;
 
@@ -129,6 +131,34 @@ __device__ __forceinline__ bool pair_live(int tid, int c) { return c < 4 || tid 
 // W_2M^(M-k) = -conj(W_2M^k)
 __device__ __forceinline__ double2 tw_mirror(double2 w) { return make_double2(-w.x, w.y); }
 
+// Morton spread: bit i of v -> bit 2 i
+__device__ __forceinline__ uint64_t spread32(uint32_t v) {
+  uint64_t x = v;
+  x = (x | (x << 16)) & 0x0000FFFF0000FFFFull;
+  x = (x | (x << 8)) & 0x00FF00FF00FF00FFull;
+  x = (x | (x << 4)) & 0x0F0F0F0F0F0F0F0Full;
+  x = (x | (x << 2)) & 0x3333333333333333ull;
+  x = (x | (x << 1)) & 0x5555555555555555ull;
+  return x;
+}
+
+// Store a channel's kept samples [BLOCKCUT, BLOCKCUT + copylen) from the chunk
+// layout in LDS (pair m = t + 1024 q per lane: coalesced 16-byte stores).
+// o is indexed by block position.
+__device__ __forceinline__ void store_chan(const double2* sx, double* o, int t, int copylen) {
+#pragma unroll
+  for (int q = 0; q < 8; q++) {
+    const int m = t + 1024 * q;
+    const int p = 2 * m;
+    const double2 z = sx[SWC(m)];
+    const bool in0 = p >= BLOCKCUT && p < BLOCKCUT + copylen;
+    const bool in1 = p + 1 >= BLOCKCUT && p + 1 < BLOCKCUT + copylen;
+    if (in0 && in1) *reinterpret_cast<double2*>(o + p) = z;
+    else if (in0) o[p] = z.x;
+    else if (in1) o[p + 1] = z.y;
+  }
+}
+
 struct Pairs {
   double2 a[5], b[5];   // value at k and at M-k of each pair slot
 };
@@ -191,14 +221,15 @@ __device__ unsigned long long g_stamps[LDG_STAMP_BLOCKS][32];
 extern "C" __global__ __launch_bounds__(1024) void ldg_k_demod(
     const int32_t* __restrict__ smap, const ReadDesc* __restrict__ reads, const uint8_t* __restrict__ cap, int64_t cap_first, int64_t cap_nsamp,
     int fmt, const double2* __restrict__ tw, const double2* __restrict__ twk, const double2* __restrict__ rf_filt,
-    const double2* __restrict__ g_video, const double2* __restrict__ g_05, const double2* __restrict__ g_burst,
-    const double2* __restrict__ g_pilot, const double2* __restrict__ g_psync,
+    const double2* __restrict__ g_video, const double2* __restrict__ g_05, const double* __restrict__ iir,
     const double2* __restrict__ a_lfilt, const double2* __restrict__ a_rfilt, SysConst C,
     double* __restrict__ video, int64_t vread_stride, int64_t vchan_stride,
     double* __restrict__ audio1, int64_t aread_stride, int64_t achan_stride, int32_t* __restrict__ status,
     double2* __restrict__ ospill, SyncTile* __restrict__ stiles, double2* __restrict__ aslice,
     unsigned long long* __restrict__ span) {
   __shared__ double2 s_x[M];          // 128 KiB: the 8192-point transforms
+  __shared__ uint64_t s_bits[BLOCKLEN / 64];   // sync detector bits
+  __shared__ IIRAux s_aux;
   const CBuf X_{s_x};
   const int tid = threadIdx.x;
   STAMP(0);
@@ -364,94 +395,139 @@ extern "C" __global__ __launch_bounds__(1024) void ldg_k_demod(
   __syncthreads();
   STAMP(11);
 
-  // ---- 6. output channels: video, burst, [pilot], 0.5 MHz (its output is the
-  // sync detector's input), then sync from the detector's own spectrum.  One
-  // loop body: one copy of the inverse FFT in the code.
+  // ---- 6. output channels.
+  //  a. demod_05 = C2R(D * FVideo05), rolled by -32 (lddecode_core.py:302-303),
+  //     and its sync detector bits inrange(., iretohz(-55), iretohz(-25)) (:308)
+  //     into an LDS bitmask;
+  //  b. demod_sync: ifft(fft(bits) * FPsync) (:310) as the periodic recurrence
+  //     of FPsync's butter(1) design (iir.hpp), not two more transforms;
+  //  c. demod = C2R(D * FVideo);
+  //  d. demod_burst (and PAL demod_pilot): FVideoBurst = FVideo * Fburst
+  //     (:204-209), so the periodic recurrence of Fburst over demod (iir.hpp).
   const double inv = 1.0 / (double)M;
-  const int nout = C.n_chan > 4 ? 5 : 4;
-#pragma clang loop unroll(disable)
-  for (int e = 0; e < nout; e++) {
-    const int kind = (C.n_chan > 4 || e < 2) ? e : e + 1;   // 0 video, 1 burst, 2 pilot, 3 0.5 MHz, 4 sync
-    const double2* G = kind == 0 ? g_video : kind == 1 ? g_burst : kind == 2 ? g_pilot : kind == 3 ? g_05 : g_psync;
-    merge_pairs(X_, twk, G, tid, D);
-    STAMP(12 + 3 * e);
+  double2* sx = s_x;                             // chunk layout SWC (iir.hpp) from here on
+  {
+    merge_pairs(X_, twk, g_05, tid, D);
+    STAMP(12);
     double2 zr[8];                               // outputs at natural positions t + T q
     fft8k_dit<true, true>(s_x, tw, tid, zr);
-    STAMP(13 + 3 * e);
+    STAMP(13);
     const int t = fresh(tid);
-    if (kind != 3) {
-      const int ch = kind == 0 ? CH_DEMOD : kind == 1 ? CH_BURST : kind == 2 ? CH_PILOT : CH_SYNC;
-      double* o = vout + (int64_t)ch * vchan_stride;
+    double* o = vout + (int64_t)CH_05 * vchan_stride;
 #pragma unroll
-      for (int q = 0; q < 8; q++) {
-        const int m = t + T * q;
-        const int p = 2 * m;
-        const double2 z = zr[q];
-        const bool in0 = p >= BLOCKCUT && p < BLOCKCUT + copylen;
-        const bool in1 = p + 1 >= BLOCKCUT && p + 1 < BLOCKCUT + copylen;
-        if (in0 && in1) *reinterpret_cast<double2*>(o + p) = make_double2(z.x * inv, z.y * inv);
-        else if (in0) o[p] = z.x * inv;
-        else if (in1) o[p + 1] = z.y * inv;
+    for (int q = 0; q < 8; q++) {
+      const int m = t + T * q;
+      const double v0 = zr[q].x * inv, v1 = zr[q].y * inv;
+      // value at block position p lands at rolled position (p - 32) mod 16384 (even: p0 + 1 never wraps)
+      const int p0 = (2 * m - BLOCKCUT_END) & (BLOCKLEN - 1);
+      const bool in0 = p0 >= BLOCKCUT && p0 < BLOCKCUT + copylen;
+      const bool in1 = p0 + 1 >= BLOCKCUT && p0 + 1 < BLOCKCUT + copylen;
+      if (in0 && in1) *reinterpret_cast<double2*>(o + p0) = make_double2(v0, v1);
+      else if (in0) o[p0] = v0;
+      else if (in1) o[p0 + 1] = v1;
+      // detector bits at UNROLLED block positions 2m, 2m + 1: wave w covers
+      // positions [2048 q + 128 w, +128) = two 64-bit words, even/odd lanes interleaved
+      const uint64_t be = __ballot(v0 >= C.sync_lo && v0 <= C.sync_hi);
+      const uint64_t bo = __ballot(v1 >= C.sync_lo && v1 <= C.sync_hi);
+      if ((t & 63) == 0) {
+        const int wd = 32 * q + 2 * (t >> 6);
+        s_bits[wd] = spread32((uint32_t)be) | (spread32((uint32_t)bo) << 1);
+        s_bits[wd + 1] = spread32((uint32_t)(be >> 32)) | (spread32((uint32_t)(bo >> 32)) << 1);
       }
-      if (kind == 4) {
-#pragma unroll
-        for (int q = 0; q < 8; q++) X_[t + T * q] = zr[q];
-        __syncthreads();
-        // sync tiles (common.hpp SyncTile): tile j of this block = outputs
-        // [off + 32 j, +32) = block positions [1024 + 32 j, +32) = pairs
-        // m in [512 + 16 j, +16); threads 2j and 2j+1 scan one half each in
-        // order, then the halves combine (np.argmax order: the lower half wins ties)
-        const int j = t >> 1, hf = t & 1;
-        const int ntile = (copylen + 31) / 32;
-        double v = -__builtin_inf();
-        int64_t vi = 0x7fffffffffffffffLL;
-        const int64_t n0 = (int64_t)off + 32 * j;
-        if (j < ntile) {
-#pragma unroll
-          for (int r = 0; r < 8; r++) {
-            const double2 z = X_[512 + 16 * j + 8 * hf + r];
-            const int e = 16 * hf + 2 * r;
-            if (e < copylen - 32 * j && am_beats(z.x * inv, n0 + e, v, vi)) { v = z.x * inv; vi = n0 + e; }
-            if (e + 1 < copylen - 32 * j && am_beats(z.y * inv, n0 + e + 1, v, vi)) { v = z.y * inv; vi = n0 + e + 1; }
-          }
-        }
-        const double ov = __shfl_xor(v, 1);
-        const int64_t oi = __shfl_xor(vi, 1);
-        if (am_beats(ov, oi, v, vi)) { v = ov; vi = oi; }
-        if (j < ntile && hf == 0) {
-          SyncTile tt;
-          tt.v = v;
-          tt.idx = vi;
-          stiles[(int64_t)slot * STILE_PER_SLOT + (n0 >> 5)] = tt;
-        }
-      }
-      __syncthreads();
-    } else {
-      double v0[8], v1[8];
-#pragma unroll
-      for (int q = 0; q < 8; q++) { const double2 z = zr[q]; v0[q] = z.x * inv; v1[q] = z.y * inv; }
-      double* o = vout + (int64_t)CH_05 * vchan_stride;
-#pragma unroll
-      for (int q = 0; q < 8; q++) {
-        const int m = t + T * q;
-        // value at block position p lands at rolled position (p - 32) mod 16384 (even: p0 + 1 never wraps)
-        const int p0 = (2 * m - BLOCKCUT_END) & (BLOCKLEN - 1);
-        const bool in0 = p0 >= BLOCKCUT && p0 < BLOCKCUT + copylen;
-        const bool in1 = p0 + 1 >= BLOCKCUT && p0 + 1 < BLOCKCUT + copylen;
-        if (in0 && in1) *reinterpret_cast<double2*>(o + p0) = make_double2(v0[q], v1[q]);
-        else if (in0) o[p0] = v0[q];
-        else if (in1) o[p0 + 1] = v1[q];
-        // inrange(demod_05, iretohz(-55), iretohz(-25)) as 0/1 doubles
-        const int mz = (m - BLOCKCUT_END / 2) & (M - 1);
-        X_[mz] = make_double2((v0[q] >= C.sync_lo && v0[q] <= C.sync_hi) ? 1.0 : 0.0,
-                              (v1[q] >= C.sync_lo && v1[q] <= C.sync_hi) ? 1.0 : 0.0);
-      }
-      fft8k_dif<false>(s_x, tw, tid);
-      split_pairs(X_, twk, tid, D);
-      __syncthreads();
     }
-    STAMP(14 + 3 * e);
   }
+  __syncthreads();
+  STAMP(14);
+  {
+    // sync: thread t owns ROLLED positions [16 t, 16 t + 16) = unrolled [16 t + 32, +16)
+    const int t = fresh(tid);
+    const uint16_t* hb = reinterpret_cast<const uint16_t*>(s_bits);
+    const uint32_t cur = hb[(t + 2) & 1023], prv = hb[(t + 1) & 1023] >> 15;
+    double y[IIR_CHUNK];
+    iir1_bits(cur, prv, iir, &s_aux, t, y);
+    // sync tiles (common.hpp SyncTile): tile j = outputs [off + 32 j, +32) =
+    // block positions [1024 + 32 j, +32) = chunks of threads 64 + 2 j (+1); np.argmax
+    // order, the lower half wins ties
+    {
+      const int j = (t >> 1) - 32, hf = t & 1;
+      const int ntile = (copylen + 31) / 32;
+      double v = -__builtin_inf();
+      int64_t vi = 0x7fffffffffffffffLL;
+      const int64_t n0 = (int64_t)off + 32 * j;
+      if (j >= 0 && j < ntile) {
+#pragma unroll
+        for (int i = 0; i < IIR_CHUNK; i++) {
+          const int e = 16 * hf + i;
+          if (e < copylen - 32 * j && am_beats(y[i], n0 + e, v, vi)) { v = y[i]; vi = n0 + e; }
+        }
+      }
+      const double ov = __shfl_xor(v, 1);
+      const int64_t oi = __shfl_xor(vi, 1);
+      if (am_beats(ov, oi, v, vi)) { v = ov; vi = oi; }
+      if (j >= 0 && j < ntile && hf == 0) {
+        SyncTile tt;
+        tt.v = v;
+        tt.idx = vi;
+        stiles[(int64_t)slot * STILE_PER_SLOT + (n0 >> 5)] = tt;
+      }
+    }
+#pragma unroll
+    for (int c = 0; c < 8; c++) sx[SWC(8 * t + c)] = make_double2(y[2 * c], y[2 * c + 1]);
+  }
+  __syncthreads();
+  store_chan(sx, vout + (int64_t)CH_SYNC * vchan_stride, tid, copylen);
+  __syncthreads();
+  STAMP(15);
+  {
+    merge_pairs(X_, twk, g_video, tid, D);
+    STAMP(16);
+    double2 zr[8];
+    fft8k_dit<true, true>(s_x, tw, tid, zr);
+    STAMP(17);
+    const int t = fresh(tid);
+    double* o = vout + (int64_t)CH_DEMOD * vchan_stride;
+#pragma unroll
+    for (int q = 0; q < 8; q++) {
+      const int m = t + T * q;
+      const int p = 2 * m;
+      const double2 z = make_double2(zr[q].x * inv, zr[q].y * inv);
+      sx[SWC(m)] = z;
+      const bool in0 = p >= BLOCKCUT && p < BLOCKCUT + copylen;
+      const bool in1 = p + 1 >= BLOCKCUT && p + 1 < BLOCKCUT + copylen;
+      if (in0 && in1) *reinterpret_cast<double2*>(o + p) = z;
+      else if (in0) o[p] = z.x;
+      else if (in1) o[p + 1] = z.y;
+    }
+  }
+  __syncthreads();
+  STAMP(18);
+  {
+    const int t = fresh(tid);
+    double x[IIR_CHUNK];
+#pragma unroll
+    for (int c = 0; c < 8; c++) {
+      const double2 z = sx[SWC(8 * t + c)];
+      x[2 * c] = z.x;
+      x[2 * c + 1] = z.y;
+    }
+    const double2 h = sx[SWC((8 * t - 1) & (M - 1))];
+    double y[IIR_CHUNK];
+    iir2(x, h.y, h.x, iir + 3, iir + IIR_MB, &s_aux, t, y);
+#pragma unroll
+    for (int c = 0; c < 8; c++) sx[SWC(8 * t + c)] = make_double2(y[2 * c], y[2 * c + 1]);
+    __syncthreads();
+    store_chan(sx, vout + (int64_t)CH_BURST * vchan_stride, t, copylen);
+    if (C.n_chan > 4) {
+      // pilot from the same demod samples (still in x); iir2's barriers order
+      // the burst stores' LDS reads before the writes below
+      iir2(x, h.y, h.x, iir + 8, iir + IIR_MP, &s_aux, t, y);
+#pragma unroll
+      for (int c = 0; c < 8; c++) sx[SWC(8 * t + c)] = make_double2(y[2 * c], y[2 * c + 1]);
+      __syncthreads();
+      store_chan(sx, vout + (int64_t)CH_PILOT * vchan_stride, t, copylen);
+    }
+  }
+  STAMP(19);
   if (span && tid == 0) atomicMax(&span[1], (unsigned long long)__builtin_amdgcn_s_memrealtime());
 }
 

@@ -64,7 +64,7 @@ _DP = C.POINTER(C.c_double)
 
 class Filters(C.Structure):
     _fields_ = [(k, _DP) for k in ('rfvideo', 'mtf', 'fvideo', 'fvideo05', 'fvideoburst', 'fvideopilot', 'fpsync',
-                                   'audio_lfilt', 'audio_rfilt', 'audio_lpf2', 'mtf_logabs', 'mtf_arg')]
+                                   'audio_lfilt', 'audio_rfilt', 'audio_lpf2', 'mtf_logabs', 'mtf_arg', 'iir')]
 
 
 _lib = None

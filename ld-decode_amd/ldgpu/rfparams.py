@@ -97,19 +97,27 @@ class RFTables:
         tb, ta = sps.zpk2tf([-d1 * 1e-10], [-d0 * 1e-10], d0 / d1)
         deemp = _whole(sps.bilinear(tb, ta, 1.0 / nyq))
         f05 = _whole((sps.firwin(65, [0.5 / nyq_mhz], pass_zero=True), [1.0]))
-        burst = _whole(sps.butter(1, [(S.fsc_mhz - .1) / nyq_mhz, (S.fsc_mhz + .1) / nyq_mhz], btype='bandpass'))
+        burst_ba = sps.butter(1, [(S.fsc_mhz - .1) / nyq_mhz, (S.fsc_mhz + .1) / nyq_mhz], btype='bandpass')
+        burst = _whole(burst_ba)
+        psync_ba = sps.butter(1, 0.05 / nyq_mhz, btype='low')
+        pilot_ba = sps.butter(1, [3.7 / nyq_mhz, 3.8 / nyq_mhz], btype='bandpass') if S.name == 'PAL' else None
         self.tables = {
             'rfvideo': rfv, 'mtf': mtf,
             'fvideo': lpf * deemp,
             'fvideo05': lpf * deemp * f05,
             'fvideoburst': lpf * deemp * burst,
-            'fpsync': _whole(sps.butter(1, 0.05 / nyq_mhz, btype='low')),
+            'fpsync': _whole(psync_ba),
             'mtf_logabs': np.log(np.abs(mtf)),
             'mtf_arg': np.angle(mtf),
         }
         if S.name == 'PAL':
-            pilot = _whole(sps.butter(1, [3.7 / nyq_mhz, 3.8 / nyq_mhz], btype='bandpass'))
-            self.tables['fvideopilot'] = lpf * deemp * pilot
+            self.tables['fvideopilot'] = lpf * deemp * _whole(pilot_ba)
+        # the butter(1) designs behind fpsync / Fburst / Fpilot (a[0] == 1): the demod
+        # runs these three channels as periodic recurrences (csrc/iir.hpp)
+        iir = [psync_ba[0][0], psync_ba[0][1], psync_ba[1][1],
+               *burst_ba[0], *burst_ba[1][1:]]
+        iir += ([*pilot_ba[0], *pilot_ba[1][1:]] if pilot_ba is not None else [0.0] * 5)
+        self.tables['iir'] = np.array(iir, np.float64)
 
         # audio (lddecode_core.py:223-279)
         fdiv1 = 32 if inputfreq >= 32 else 16
