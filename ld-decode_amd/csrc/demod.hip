@@ -131,26 +131,22 @@ __device__ __forceinline__ bool pair_live(int tid, int c) { return c < 4 || tid 
 // W_2M^(M-k) = -conj(W_2M^k)
 __device__ __forceinline__ double2 tw_mirror(double2 w) { return make_double2(-w.x, w.y); }
 
-// Morton spread: bit i of v -> bit 2 i
-__device__ __forceinline__ uint64_t spread32(uint32_t v) {
-  uint64_t x = v;
-  x = (x | (x << 16)) & 0x0000FFFF0000FFFFull;
-  x = (x | (x << 8)) & 0x00FF00FF00FF00FFull;
-  x = (x | (x << 4)) & 0x0F0F0F0F0F0F0F0Full;
-  x = (x | (x << 2)) & 0x3333333333333333ull;
-  x = (x | (x << 1)) & 0x5555555555555555ull;
-  return x;
-}
+// Timing probe only (-DLDG_PROBE_NOSTORE): the channel stores are skipped, results are garbage.
+#ifdef LDG_PROBE_NOSTORE
+constexpr bool kProbeNoStore = true;
+#else
+constexpr bool kProbeNoStore = false;
+#endif
 
-// Store a channel's kept samples [BLOCKCUT, BLOCKCUT + copylen) from the chunk
-// layout in LDS (pair m = t + 1024 q per lane: coalesced 16-byte stores).
-// o is indexed by block position.
-__device__ __forceinline__ void store_chan(const double2* sx, double* o, int t, int copylen) {
-#pragma unroll
-  for (int q = 0; q < 8; q++) {
-    const int m = t + 1024 * q;
-    const int p = 2 * m;
-    const double2 z = sx[SWC(m)];
+// Store the pair of samples 2m, 2m+1 of a channel (o indexed by block position)
+// if kept ([BLOCKCUT, BLOCKCUT + copylen)); the wave-uniform test keeps the
+// common case (a wave's 64 pairs all kept or all dropped) branch-free.
+__device__ __forceinline__ void store_pair(double* o, int m, double2 z, int copylen) {
+  const int p = 2 * m;
+  const int pw0 = 2 * (m & ~63);
+  if (pw0 >= BLOCKCUT && pw0 + 127 < BLOCKCUT + copylen) {
+    *reinterpret_cast<double2*>(o + p) = z;
+  } else if (pw0 + 127 >= BLOCKCUT && pw0 < BLOCKCUT + copylen) {
     const bool in0 = p >= BLOCKCUT && p < BLOCKCUT + copylen;
     const bool in1 = p + 1 >= BLOCKCUT && p + 1 < BLOCKCUT + copylen;
     if (in0 && in1) *reinterpret_cast<double2*>(o + p) = z;
@@ -158,6 +154,67 @@ __device__ __forceinline__ void store_chan(const double2* sx, double* o, int t, 
     else if (in1) o[p + 1] = z.y;
   }
 }
+
+// Store a channel's kept samples [BLOCKCUT, BLOCKCUT + copylen) from the chunk
+// layout in LDS (pair m = t + 1024 q per lane: coalesced 16-byte stores).
+// o is indexed by block position.
+__device__ __forceinline__ void store_chan(const double2* sx, double* o, int t, int copylen) {
+  if (kProbeNoStore) return;
+#pragma unroll
+  for (int q = 0; q < 8; q++) {
+    const int m = t + 1024 * q;
+    store_pair(o, m, sx[SWC(m)], copylen);
+  }
+}
+
+// atan(i / 64), i = 0..64 (the fast_atan2 table; copied to LDS per workgroup)
+__constant__ double c_atan64[65] = {
+    0.0, 0.015623728620476831, 0.031239833430268277, 0.046840712915969654,
+    0.06241880999595735, 0.0779666338315423, 0.09347678115858947, 0.1089419569898658,
+    0.12435499454676144, 0.13970887428916365, 0.15499674192394097, 0.1702119252854744,
+    0.18534794999569476, 0.2003985538258785, 0.21535769969773805, 0.23021958727684372,
+    0.24497866312686414, 0.2596296294082575, 0.2741674511196588, 0.2885873618940774,
+    0.3028848683749714, 0.31705575320914703, 0.3310960767041321, 0.34500217720710513,
+    0.35877067027057225, 0.3723984466767542, 0.38588266939807375, 0.39922076957525254,
+    0.4124104415973873, 0.42544963737004227, 0.43833655985795783, 0.4510696559885235,
+    0.4636476090008061, 0.4760693303227612, 0.48833395105640554, 0.5004408131472942,
+    0.5123894603107377, 0.5241796287829132, 0.5358112379604637, 0.5472843809874369,
+    0.5585993153435624, 0.5697564534829784, 0.5807563535676704, 0.5915997103351114,
+    0.6022873461349642, 0.6128202021652414, 0.6231993299340659, 0.6334258829691446,
+    0.6435011087932844, 0.6534263411807619, 0.6632029927060933, 0.6728325475937632,
+    0.6823165548747481, 0.6916566218531999, 0.7008544078844502, 0.7099116184635249,
+    0.7188299996216245, 0.7276113326265107, 0.7362574289814281, 0.7447701257160751,
+    0.7531512809621944, 0.7614027698055784, 0.7695264804056583, 0.7775243103733478,
+    0.7853981633974483};
+
+// np.angle(y + i x) = atan2(y, x) in (-pi, pi] for the FM demod (lddutils.py:320-334),
+// FP64, max abs error 4.4e-16 rad (2e7 random points against libm, incl. axes and
+// zeros; atan2(+-0, -0) returns +-0, not +-pi).  About a third of the
+// instructions of the library atan2: r = min/max of |x|, |y| is rounded to
+// c = i/64, atan(r) = atan(c) + atan(t), t = (r - c) / (1 + r c) = (n - c d)/(d + c n),
+// |t| <= 1/128, so atan(t) to O(t^9) = 1e-20 is t - t^3/3 + t^5/5 - t^7/7.
+__device__ __forceinline__ double fast_atan2(double y, double x, const double* s_atan) {
+  const double ax = fabs(x), ay = fabs(y);
+  const bool sw = ay > ax;
+  const double num = sw ? ax : ay, den = sw ? ay : ax;
+  const bool zero = !(den > 0.0);
+  int i = (int)__builtin_rint(num * __builtin_amdgcn_rcp(den) * 64.0);
+  i = zero ? 0 : min(max(i, 0), 64);
+  const double c = (double)i * (1.0 / 64);
+  const double n = __fma_rn(-c, den, num);
+  const double d = __fma_rn(c, num, den);
+  double r = __builtin_amdgcn_rcp(d);
+  r = __fma_rn(r, __fma_rn(-d, r, 1.0), r);
+  const double t = zero ? 0.0 : n * r;
+  const double t2 = t * t;
+  const double pl = __fma_rn(__fma_rn(-1.0 / 7, t2, 1.0 / 5), t2, -1.0 / 3);
+  double th = s_atan[i] + __fma_rn(t * t2, pl, t);
+  if (sw) th = 1.57079632679489661923 - th;
+  if (x < 0.0) th = 3.14159265358979323846 - th;
+  return copysign(th, y);
+}
+
+constexpr bool kFastAtan2 = false;
 
 struct Pairs {
   double2 a[5], b[5];   // value at k and at M-k of each pair slot
@@ -217,7 +274,7 @@ __device__ unsigned long long g_stamps[LDG_STAMP_BLOCKS][32];
 
 // grid: n_reads * MAX_BLOCKS_PER_READ workgroups of 1024 threads.
 // ospill: 10 x 1024 double2 per workgroup (the odd-half analytic spectrum is
-// parked there, coalesced, while the even half is transformed).
+// parked in its first 8192 entries while the even half is transformed).
 extern "C" __global__ __launch_bounds__(1024) void ldg_k_demod(
     const int32_t* __restrict__ smap, const ReadDesc* __restrict__ reads, const uint8_t* __restrict__ cap, int64_t cap_first, int64_t cap_nsamp,
     int fmt, const double2* __restrict__ tw, const double2* __restrict__ twk, const double2* __restrict__ rf_filt,
@@ -228,10 +285,12 @@ extern "C" __global__ __launch_bounds__(1024) void ldg_k_demod(
     double2* __restrict__ ospill, SyncTile* __restrict__ stiles, double2* __restrict__ aslice,
     unsigned long long* __restrict__ span) {
   __shared__ double2 s_x[M];          // 128 KiB: the 8192-point transforms
-  __shared__ uint64_t s_bits[BLOCKLEN / 64];   // sync detector bits
+  __shared__ __align__(16) uint8_t s_flag[BLOCKLEN];   // sync detector bits, one byte per sample
   __shared__ IIRAux s_aux;
+  __shared__ double s_atan[65];
   const CBuf X_{s_x};
   const int tid = threadIdx.x;
+  if (tid < 65) s_atan[tid] = c_atan64[tid];   // ordered by the first transform's barrier
   STAMP(0);
   // profiling: the launch's execution span on the constant-rate clock (first
   // workgroup start, last workgroup end), what a kernel trace reports
@@ -251,7 +310,9 @@ extern "C" __global__ __launch_bounds__(1024) void ldg_k_demod(
   }
   double* vout = video + (int64_t)slot * vread_stride + off - BLOCKCUT;   // index by block position p
   const double2* F = rf_filt + (int64_t)rd.filt_slot * BLOCKLEN;
-  double2* osp = ospill + (int64_t)blockIdx.x * 10 * T + tid;
+  // odd-half park, in LDS image order (park[u] = the value for LDS slot u), so
+  // it returns to LDS by LDS-DMA (global_load_lds) without a register pass
+  double2* park = ospill + (int64_t)blockIdx.x * 10 * T;
   constexpr double TAU = 6.283185307179586;
 
   // ---- 1. raw samples -> z[m] = x[2m] + i x[2m+1]; forward FFT ---------------
@@ -322,12 +383,12 @@ extern "C" __global__ __launch_bounds__(1024) void ldg_k_demod(
       const double2 yk = cmul(X.a[c], F[sl.p]);
       const double2 yk2 = cmul(conj2(X.b[c]), F[M + sl.p]);
       X_[sl.p] = cadd(yk, yk2);
-      osp[(2 * c) * T] = cmulc(csub(yk, yk2), wk);
+      park[SW(sl.p)] = cmulc(csub(yk, yk2), wk);
       if (sl.pp != sl.p) {
         const double2 ykp = cmul(X.b[c], F[sl.pp]);
         const double2 ykp2 = cmul(conj2(X.a[c]), F[M + sl.pp]);
         X_[sl.pp] = cadd(ykp, ykp2);
-        osp[(2 * c + 1) * T] = cmulc(csub(ykp, ykp2), tw_mirror(wk));
+        park[SW(sl.pp)] = cmulc(csub(ykp, ykp2), tw_mirror(wk));
       }
     }
   }
@@ -336,34 +397,36 @@ extern "C" __global__ __launch_bounds__(1024) void ldg_k_demod(
   // (audio phase 1 -- 2 x IFFT1024 -> FM demod -- runs in ldg_k_audio1 on the
   // slices above: the demod keeps 128 KiB of LDS, so kernels with up to 32 KiB
   // share its CUs)
-  STAMP(4);
   // ---- 4. analytic IFFTs (even, odd) -> instantaneous phase --------------------
   // One loop body for both halves: one copy of the inverse FFT in the code (the
   // kernel would outgrow the instruction cache with every transform inlined).
   double the[8], tho[8];
 #pragma clang loop unroll(disable)
   for (int h = 0; h < 2; h++) {
-    if (h) {
-      const int t = fresh(tid);
-#pragma unroll
-      for (int c = 0; c < 5; c++) {
-        if (!pair_live(t, c)) continue;
-        const Slot sl = slot_of(t, c);
-        X_[sl.p] = osp[(2 * c) * T];
-        if (sl.pp != sl.p) X_[sl.pp] = osp[(2 * c + 1) * T];
-      }
-    }
-    STAMP(5 + h);
+    STAMP(4 + 2 * h);
     double2 zr[8];
     fft8k_dit<true, true>(s_x, tw, tid, zr);
-    STAMP(6 + h);
+    if (h == 0) {
+      // the odd half returns to LDS while the even half's angles are computed:
+      // every wave's park stores are complete (vmcnt) before any wave reads them
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      const int t = fresh(tid);
+      const int wbase = __builtin_amdgcn_readfirstlane(t & ~63);
+#pragma unroll
+      for (int i = 0; i < 8; i++)
+        __builtin_amdgcn_global_load_lds((const void*)(park + T * i + t),
+                                         (__attribute__((address_space(3))) void*)(s_x + T * i + wbase), 16, 0, 0);
+    }
+    STAMP(5 + 2 * h);
 #pragma unroll
     for (int q = 0; q < 8; q++) {
       const double2 z = zr[q];
-      const double a = atan2(z.y, z.x);
+      const double a = kFastAtan2 ? fast_atan2(z.y, z.x, s_atan) : atan2(z.y, z.x);
       if (h) tho[q] = a;
       else the[q] = a;
     }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
   }
   double* ph = reinterpret_cast<double*>(s_x);    // plain (unswizzled) phase scratch
@@ -422,18 +485,21 @@ extern "C" __global__ __launch_bounds__(1024) void ldg_k_demod(
       const int p0 = (2 * m - BLOCKCUT_END) & (BLOCKLEN - 1);
       const bool in0 = p0 >= BLOCKCUT && p0 < BLOCKCUT + copylen;
       const bool in1 = p0 + 1 >= BLOCKCUT && p0 + 1 < BLOCKCUT + copylen;
-      if (in0 && in1) *reinterpret_cast<double2*>(o + p0) = make_double2(v0, v1);
-      else if (in0) o[p0] = v0;
-      else if (in1) o[p0 + 1] = v1;
-      // detector bits at UNROLLED block positions 2m, 2m + 1: wave w covers
-      // positions [2048 q + 128 w, +128) = two 64-bit words, even/odd lanes interleaved
-      const uint64_t be = __ballot(v0 >= C.sync_lo && v0 <= C.sync_hi);
-      const uint64_t bo = __ballot(v1 >= C.sync_lo && v1 <= C.sync_hi);
-      if ((t & 63) == 0) {
-        const int wd = 32 * q + 2 * (t >> 6);
-        s_bits[wd] = spread32((uint32_t)be) | (spread32((uint32_t)bo) << 1);
-        s_bits[wd + 1] = spread32((uint32_t)(be >> 32)) | (spread32((uint32_t)(bo >> 32)) << 1);
+      if (!kProbeNoStore) {
+        // the wave's 64 pairs are all kept or all dropped except at the block ends
+        const int pw0 = (2 * (m & ~63) - BLOCKCUT_END) & (BLOCKLEN - 1);
+        if (pw0 >= BLOCKCUT && pw0 + 127 < BLOCKCUT + copylen) {
+          *reinterpret_cast<double2*>(o + p0) = make_double2(v0, v1);
+        } else {
+          if (in0 && in1) *reinterpret_cast<double2*>(o + p0) = make_double2(v0, v1);
+          else if (in0) o[p0] = v0;
+          else if (in1) o[p0 + 1] = v1;
+        }
       }
+      // detector flags at UNROLLED block positions 2m, 2m + 1
+      const uint32_t f0 = (v0 >= C.sync_lo && v0 <= C.sync_hi) ? 1u : 0u;
+      const uint32_t f1 = (v1 >= C.sync_lo && v1 <= C.sync_hi) ? 1u : 0u;
+      *reinterpret_cast<uint16_t*>(s_flag + 2 * m) = (uint16_t)(f0 | (f1 << 8));
     }
   }
   __syncthreads();
@@ -441,8 +507,14 @@ extern "C" __global__ __launch_bounds__(1024) void ldg_k_demod(
   {
     // sync: thread t owns ROLLED positions [16 t, 16 t + 16) = unrolled [16 t + 32, +16)
     const int t = fresh(tid);
-    const uint16_t* hb = reinterpret_cast<const uint16_t*>(s_bits);
-    const uint32_t cur = hb[(t + 2) & 1023], prv = hb[(t + 1) & 1023] >> 15;
+    const uint4 fl = *reinterpret_cast<const uint4*>(s_flag + ((16 * t + 32) & (BLOCKLEN - 1)));
+    const uint32_t prv = s_flag[(16 * t + 31) & (BLOCKLEN - 1)];
+    uint32_t cur = 0;
+    {
+      const uint32_t w[4] = {fl.x, fl.y, fl.z, fl.w};
+#pragma unroll
+      for (int i = 0; i < 16; i++) cur |= ((w[i >> 2] >> (8 * (i & 3))) & 1u) << i;
+    }
     double y[IIR_CHUNK];
     iir1_bits(cur, prv, iir, &s_aux, t, y);
     // sync tiles (common.hpp SyncTile): tile j = outputs [off + 32 j, +32) =
@@ -489,14 +561,9 @@ extern "C" __global__ __launch_bounds__(1024) void ldg_k_demod(
 #pragma unroll
     for (int q = 0; q < 8; q++) {
       const int m = t + T * q;
-      const int p = 2 * m;
       const double2 z = make_double2(zr[q].x * inv, zr[q].y * inv);
       sx[SWC(m)] = z;
-      const bool in0 = p >= BLOCKCUT && p < BLOCKCUT + copylen;
-      const bool in1 = p + 1 >= BLOCKCUT && p + 1 < BLOCKCUT + copylen;
-      if (in0 && in1) *reinterpret_cast<double2*>(o + p) = z;
-      else if (in0) o[p] = z.x;
-      else if (in1) o[p + 1] = z.y;
+      if (!kProbeNoStore) store_pair(o, m, z, copylen);
     }
   }
   __syncthreads();

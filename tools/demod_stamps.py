@@ -14,11 +14,10 @@ import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, 'ld-decode_amd'))
 VARIANT = os.path.join(ROOT, 'ld-decode_amd', 'ldgpu', 'libldgpu_stamps.so')
-PHASES = {0: 'prologue+load', 1: 'raw FFT', 2: 'split/filter/park', 3: 'audio IFFT+atan2', 4: '-',
-          5: 'E IFFT', 6: 'O IFFT', 7: 'O atan2+phase', 8: 'FM demod', 9: 'D FFT', 10: 'D split',
-          11: 'ch0 merge', 12: 'ch0 IFFT', 13: 'ch0 store', 14: 'ch1 merge', 15: 'ch1 IFFT', 16: 'ch1 store',
-          17: 'ch2 merge', 18: 'ch2 IFFT', 19: 'ch2 store(+sync FFT)', 20: 'ch3 merge', 21: 'ch3 IFFT',
-          22: 'ch3 store', 23: 'ch4 merge', 24: 'ch4 IFFT', 25: 'ch4 store'}
+PHASES = {0: 'prologue+load', 1: 'raw FFT', 2: 'split/filter/park', 3: 'E IFFT wait', 4: 'E IFFT',
+          5: 'E atan2 + O reload', 6: 'O IFFT', 7: 'O atan2 + phase', 8: 'FM demod', 9: 'D FFT', 10: 'D split',
+          11: '05 merge', 12: '05 IFFT', 13: '05 store + bits', 14: 'sync scan + store', 15: 'video merge',
+          16: 'video IFFT', 17: 'video store', 18: 'burst scan + store'}
 
 
 def main():
