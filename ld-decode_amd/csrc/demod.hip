@@ -214,7 +214,7 @@ __device__ __forceinline__ double fast_atan2(double y, double x, const double* s
   return copysign(th, y);
 }
 
-constexpr bool kFastAtan2 = false;
+constexpr bool kFastAtan2 = true;
 
 struct Pairs {
   double2 a[5], b[5];   // value at k and at M-k of each pair slot

@@ -23,6 +23,8 @@ def main():
     t0 = time.perf_counter()
     log = []
     for r in range(reps):
+        if r == 2:
+            ctx.profile('demod')            # spans of the steady-state launches only
         a = time.perf_counter()
         ctx.decode_reads_async(starts, [1.0] * batch, sl[r % depth])
         b = time.perf_counter()
@@ -34,8 +36,11 @@ def main():
         for r, a, da, dw in log:
             print(f'rep {r:2d} async@{a:9.1f} us  async {da:7.1f} us  wait {dw:7.1f} us')
     import statistics
+    while ctx._pending:
+        ctx.decode_reads_wait()
+    nsp, tsp = ctx.profile_spans()
     per = [b[1] - a[1] for a, b in zip(log[depth:], log[depth + 1:])]
-    print(f"stages {os.environ.get('LDG_STAGES', '7')} depth {depth}: period median {statistics.median(per):.1f} us "
+    print(f"demod span {tsp / max(nsp, 1) * 1000:.1f} us/launch ({nsp}); stages {os.environ.get('LDG_STAGES', '7')} depth {depth}: period median {statistics.median(per):.1f} us "
           f"mean {statistics.mean(per):.1f} us (async {statistics.median(x[2] for x in log[depth:]):.1f}, "
           f"wait {statistics.median(x[3] for x in log[depth:]):.1f})")
     while ctx._pending:
