@@ -122,6 +122,15 @@ __device__ __forceinline__ Slot slot_of(int tid, int c) {
   return {p, pp, pp};
 }
 
+// This workgroup's physical CU: (XCC, SE, SH, CU) from HW_REG_XCC_ID / HW_REG_HW_ID
+// (gfx9 HW_ID: CU_ID [11:8], SH_ID [12], SE_ID [15:13]), < PARK_SLOTS.
+constexpr int PARK_SLOTS = 2048;
+__device__ __forceinline__ int cu_slot() {
+  const unsigned hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);
+  const unsigned xcc = __builtin_amdgcn_s_getreg((31 << 11) | 20);
+  return (int)(((xcc & 7u) << 8) | (((hw >> 13) & 7u) << 5) | (((hw >> 12) & 1u) << 4) | ((hw >> 8) & 15u));
+}
+
 // Opaque copy of tid: stops the compiler from hoisting per-lane twiddle loads
 // and addresses that repeat across the kernel's transforms (and spilling them).
 __device__ __forceinline__ int fresh(int tid) { asm volatile("" : "+v"(tid)); return tid; }
@@ -273,8 +282,7 @@ __device__ unsigned long long g_stamps[LDG_STAMP_BLOCKS][32];
 #endif
 
 // grid: n_reads * MAX_BLOCKS_PER_READ workgroups of 1024 threads.
-// ospill: 10 x 1024 double2 per workgroup (the odd-half analytic spectrum is
-// parked in its first 8192 entries while the even half is transformed).
+// ospill: PARK_SLOTS x 8192 double2, one odd-half park per physical CU.
 extern "C" __global__ __launch_bounds__(1024) void ldg_k_demod(
     const int32_t* __restrict__ smap, const ReadDesc* __restrict__ reads, const uint8_t* __restrict__ cap, int64_t cap_first, int64_t cap_nsamp,
     int fmt, const double2* __restrict__ tw, const double2* __restrict__ twk, const double2* __restrict__ rf_filt,
@@ -311,8 +319,11 @@ extern "C" __global__ __launch_bounds__(1024) void ldg_k_demod(
   double* vout = video + (int64_t)slot * vread_stride + off - BLOCKCUT;   // index by block position p
   const double2* F = rf_filt + (int64_t)rd.filt_slot * BLOCKLEN;
   // odd-half park, in LDS image order (park[u] = the value for LDS slot u), so
-  // it returns to LDS by LDS-DMA (global_load_lds) without a register pass
-  double2* park = ospill + (int64_t)blockIdx.x * 10 * T;
+  // it returns to LDS by LDS-DMA (global_load_lds) without a register pass.
+  // One park per physical CU (one demod workgroup per CU at a time: 128 KiB of
+  // LDS), so consecutive workgroups on a CU rewrite the same 128 KiB and it
+  // stays cache-resident instead of streaming 1 GB per launch through HBM.
+  double2* park = ospill + (int64_t)cu_slot() * M;
   constexpr double TAU = 6.283185307179586;
 
   // ---- 1. raw samples -> z[m] = x[2m] + i x[2m+1]; forward FFT ---------------
