@@ -293,12 +293,15 @@ extern "C" __global__ __launch_bounds__(1024) void ldg_k_demod(
     double2* __restrict__ ospill, SyncTile* __restrict__ stiles, double2* __restrict__ aslice,
     unsigned long long* __restrict__ span) {
   __shared__ double2 s_x[M];          // 128 KiB: the 8192-point transforms
-  __shared__ __align__(16) uint8_t s_flag[BLOCKLEN];   // sync detector bits, one byte per sample
+  __shared__ uint16_t s_bits[BLOCKLEN / 16];   // sync detector bits
+  __shared__ double2 s_tw[TW_LDS_N];           // per-lane FFT twiddles (fft8k.hpp)
   __shared__ IIRAux s_aux;
   __shared__ double s_atan[65];
   const CBuf X_{s_x};
   const int tid = threadIdx.x;
   if (tid < 65) s_atan[tid] = c_atan64[tid];   // ordered by the first transform's barrier
+  s_tw[tw_lds_pos(tid)] = tw[2 * tid];
+  const TwLds twl{s_tw};
   STAMP(0);
   // profiling: the launch's execution span on the constant-rate clock (first
   // workgroup start, last workgroup end), what a kernel trace reports
@@ -354,7 +357,7 @@ extern "C" __global__ __launch_bounds__(1024) void ldg_k_demod(
     }
   }
   STAMP(1);
-  fft8k_dif<false>(s_x, tw, tid);
+  fft8k_dif<false>(s_x, tw, twl, tid);
   STAMP(2);
 
   // ---- 2. analytic-signal spectra and the audio carrier slices ---------------
@@ -416,7 +419,7 @@ extern "C" __global__ __launch_bounds__(1024) void ldg_k_demod(
   for (int h = 0; h < 2; h++) {
     STAMP(4 + 2 * h);
     double2 zr[8];
-    fft8k_dit<true, true>(s_x, tw, tid, zr);
+    fft8k_dit<true, true>(s_x, tw, twl, tid, zr);
     if (h == 0) {
       // the odd half returns to LDS while the even half's angles are computed:
       // every wave's park stores are complete (vmcnt) before any wave reads them
@@ -462,7 +465,7 @@ extern "C" __global__ __launch_bounds__(1024) void ldg_k_demod(
     for (int q = 0; q < 8; q++) X_[tid + T * q] = make_double2(d0[q], d1[q]);
   }
   STAMP(9);
-  fft8k_dif<false>(s_x, tw, tid);
+  fft8k_dif<false>(s_x, tw, twl, tid);
   STAMP(10);
   Pairs D;
   split_pairs(X_, twk, tid, D);
@@ -479,14 +482,18 @@ extern "C" __global__ __launch_bounds__(1024) void ldg_k_demod(
   //  d. demod_burst (and PAL demod_pilot): FVideoBurst = FVideo * Fburst
   //     (:204-209), so the periodic recurrence of Fburst over demod (iir.hpp).
   const double inv = 1.0 / (double)M;
+  double pl1, pt1;
   double2* sx = s_x;                             // chunk layout SWC (iir.hpp) from here on
   {
     merge_pairs(X_, twk, g_05, tid, D);
     STAMP(12);
     double2 zr[8];                               // outputs at natural positions t + T q
-    fft8k_dit<true, true>(s_x, tw, tid, zr);
+    fft8k_dit<true, true>(s_x, tw, twl, tid, zr);
     STAMP(13);
     const int t = fresh(tid);
+    // the sync scan's per-lane powers, loaded ahead of this phase's stores
+    pl1 = iir[IIR_P1 + (t & 63)];
+    pt1 = iir[IIR_P1 + t];
     double* o = vout + (int64_t)CH_05 * vchan_stride;
 #pragma unroll
     for (int q = 0; q < 8; q++) {
@@ -507,10 +514,15 @@ extern "C" __global__ __launch_bounds__(1024) void ldg_k_demod(
           else if (in1) o[p0 + 1] = v1;
         }
       }
-      // detector flags at UNROLLED block positions 2m, 2m + 1
+      // detector bits at UNROLLED block positions 2m, 2m + 1; lanes 8j..8j+7 (pairs
+      // of 16 consecutive samples) OR their bits into lane 8j+7 (DPP row shifts)
       const uint32_t f0 = (v0 >= C.sync_lo && v0 <= C.sync_hi) ? 1u : 0u;
       const uint32_t f1 = (v1 >= C.sync_lo && v1 <= C.sync_hi) ? 1u : 0u;
-      *reinterpret_cast<uint16_t*>(s_flag + 2 * m) = (uint16_t)(f0 | (f1 << 8));
+      int xb = (int)((f0 | (f1 << 1)) << (2 * (t & 7)));
+      xb |= __builtin_amdgcn_mov_dpp(xb, 0x111, 0xf, 0xf, true);   // row_shr:1
+      xb |= __builtin_amdgcn_mov_dpp(xb, 0x112, 0xf, 0xf, true);   // row_shr:2
+      xb |= __builtin_amdgcn_mov_dpp(xb, 0x114, 0xf, 0xf, true);   // row_shr:4
+      if ((t & 7) == 7) s_bits[m >> 3] = (uint16_t)xb;
     }
   }
   __syncthreads();
@@ -518,16 +530,9 @@ extern "C" __global__ __launch_bounds__(1024) void ldg_k_demod(
   {
     // sync: thread t owns ROLLED positions [16 t, 16 t + 16) = unrolled [16 t + 32, +16)
     const int t = fresh(tid);
-    const uint4 fl = *reinterpret_cast<const uint4*>(s_flag + ((16 * t + 32) & (BLOCKLEN - 1)));
-    const uint32_t prv = s_flag[(16 * t + 31) & (BLOCKLEN - 1)];
-    uint32_t cur = 0;
-    {
-      const uint32_t w[4] = {fl.x, fl.y, fl.z, fl.w};
-#pragma unroll
-      for (int i = 0; i < 16; i++) cur |= ((w[i >> 2] >> (8 * (i & 3))) & 1u) << i;
-    }
+    const uint32_t cur = s_bits[(t + 2) & 1023], prv = (uint32_t)s_bits[(t + 1) & 1023] >> 15;
     double y[IIR_CHUNK];
-    iir1_bits(cur, prv, iir, &s_aux, t, y);
+    iir1_bits(cur, prv, iir, &s_aux, t, pl1, pt1, y);
     // sync tiles (common.hpp SyncTile): tile j = outputs [off + 32 j, +32) =
     // block positions [1024 + 32 j, +32) = chunks of threads 64 + 2 j (+1); np.argmax
     // order, the lower half wins ties
@@ -561,13 +566,16 @@ extern "C" __global__ __launch_bounds__(1024) void ldg_k_demod(
   store_chan(sx, vout + (int64_t)CH_SYNC * vchan_stride, tid, copylen);
   __syncthreads();
   STAMP(15);
+  double4 mlb, mtb;
   {
     merge_pairs(X_, twk, g_video, tid, D);
     STAMP(16);
     double2 zr[8];
-    fft8k_dit<true, true>(s_x, tw, tid, zr);
+    fft8k_dit<true, true>(s_x, tw, twl, tid, zr);
     STAMP(17);
     const int t = fresh(tid);
+    mlb = iir2_pow(iir + IIR_MB, t & 63);     // the burst scan's powers, ahead of the stores
+    mtb = iir2_pow(iir + IIR_MB, t);
     double* o = vout + (int64_t)CH_DEMOD * vchan_stride;
 #pragma unroll
     for (int q = 0; q < 8; q++) {
@@ -590,7 +598,7 @@ extern "C" __global__ __launch_bounds__(1024) void ldg_k_demod(
     }
     const double2 h = sx[SWC((8 * t - 1) & (M - 1))];
     double y[IIR_CHUNK];
-    iir2(x, h.y, h.x, iir + 3, iir + IIR_MB, &s_aux, t, y);
+    iir2(x, h.y, h.x, iir + 3, iir + IIR_MB, &s_aux, t, mlb, mtb, y);
 #pragma unroll
     for (int c = 0; c < 8; c++) sx[SWC(8 * t + c)] = make_double2(y[2 * c], y[2 * c + 1]);
     __syncthreads();
@@ -598,7 +606,7 @@ extern "C" __global__ __launch_bounds__(1024) void ldg_k_demod(
     if (C.n_chan > 4) {
       // pilot from the same demod samples (still in x); iir2's barriers order
       // the burst stores' LDS reads before the writes below
-      iir2(x, h.y, h.x, iir + 8, iir + IIR_MP, &s_aux, t, y);
+      iir2(x, h.y, h.x, iir + 8, iir + IIR_MP, &s_aux, t, iir2_pow(iir + IIR_MP, t & 63), iir2_pow(iir + IIR_MP, t), y);
 #pragma unroll
       for (int c = 0; c < 8; c++) sx[SWC(8 * t + c)] = make_double2(y[2 * c], y[2 * c + 1]);
       __syncthreads();

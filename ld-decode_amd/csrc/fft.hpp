@@ -80,10 +80,9 @@ template <int R, bool INV> __device__ __forceinline__ void dftR(double2* v) {
   else dft2<INV>(v[0], v[1]);
 }
 
-// v[r] *= w^r, r = 1..R-1, from w = W^st (conjugated for the inverse).
+// v[r] *= w^r, r = 1..R-1, from w1 = W^st (conjugated for the inverse).
 template <int R, bool INV>
-__device__ __forceinline__ void twiddle_row(double2* v, const double2* __restrict__ tw, int m) {
-  double2 w1 = tw[m];
+__device__ __forceinline__ void twiddle_row_w(double2* v, double2 w1) {
   if (INV) w1 = conj2(w1);
   v[1] = cmul(v[1], w1);
   if constexpr (R >= 4) {
@@ -99,6 +98,11 @@ __device__ __forceinline__ void twiddle_row(double2* v, const double2* __restric
       v[7] = cmul(v[7], cmul(w4, w3));
     }
   }
+}
+
+template <int R, bool INV>
+__device__ __forceinline__ void twiddle_row(double2* v, const double2* __restrict__ tw, int m) {
+  twiddle_row_w<R, INV>(v, tw[m]);
 }
 
 // One Stockham pass of radix R over an N-point array using threads [0, T).

@@ -34,6 +34,20 @@ __host__ __device__ __forceinline__ constexpr int dr_nat(int p) {
   return ((p >> 9) & 15) | (((p >> 6) & 7) << 4) | (((p >> 3) & 7) << 7) | ((p & 7) << 10);
 }
 
+// Per-lane twiddles W[i] = exp(-2 pi i i / 16384) of the transforms' stages, from
+// an LDS copy of the even entries i < 2048 (all a transform reads per lane:
+// 32 l, 256 m3, 2 q m2; the wave-uniform W_128^(q r) stay scalar loads of the
+// global table).  Global loads after a phase's global stores wait for those
+// stores (gfx9's vmcnt counts both), so the transforms read no global memory
+// per lane.  Entry k = i / 2 at tw_lds_pos(k): conflict-free for i = 32 l and
+// 256 m3 under ds_read_b128's lane groups.
+constexpr int TW_LDS_N = 1024;
+__host__ __device__ __forceinline__ constexpr int tw_lds_pos(int k) { return k ^ ((k >> 4) & 15) ^ ((k >> 7) & 7); }
+struct TwLds {
+  const double2* t;   // LDS, TW_LDS_N entries
+  __device__ __forceinline__ double2 operator()(int i) const { return t[tw_lds_pos(i >> 1)]; }
+};
+
 // a * W16^r (conjugate twiddle for the inverse), r = 0..7
 template <bool INV> __device__ __forceinline__ double2 w16(double2 a, int r) {
   constexpr double C1 = 0.92387953251128675613, S1 = 0.38268343236508977173, R2 = 0.70710678118654752440;
@@ -59,9 +73,9 @@ __device__ __forceinline__ void wave_lds_sync() {
 
 // stage-1 twiddle for the 8 points m2 + 64 r of sub-array q: v[r] *= W_8192^(q (m2 + 64 r))
 template <bool INV>
-__device__ __forceinline__ void stage1_twiddle(double2* v, const double2* __restrict__ tw, int q, int m2) {
+__device__ __forceinline__ void stage1_twiddle(double2* v, const double2* __restrict__ tw, TwLds twl, int q, int m2) {
   if (q == 0) return;   // wave-uniform
-  double2 g = tw[2 * q * m2];
+  double2 g = twl(2 * q * m2);
   if (INV) g = conj2(g);
   v[0] = cmul(v[0], g);
 #pragma unroll
@@ -75,7 +89,7 @@ __device__ __forceinline__ void stage1_twiddle(double2* v, const double2* __rest
 // Forward (INV=false) or inverse transform, natural order in, digit-reversed out.
 // Begins and ends with a workgroup barrier, like fft_lds.
 template <bool INV>
-__device__ __forceinline__ void fft8k_dif(double2* __restrict__ s, const double2* __restrict__ tw, int tid) {
+__device__ __forceinline__ void fft8k_dif(double2* __restrict__ s, const double2* __restrict__ tw, TwLds twl, int tid) {
   __syncthreads();
   {
     // stage 1: radix-16 over stride 512.  Thread pair (m, b): both read all 16
@@ -107,9 +121,9 @@ __device__ __forceinline__ void fft8k_dif(double2* __restrict__ s, const double2
     double2* p = sub + SW(l);
 #pragma unroll
     for (int r = 0; r < 8; r++) v[r] = p[64 * r];
-    stage1_twiddle<INV>(v, tw, q, l);
+    stage1_twiddle<INV>(v, tw, twl, q, l);
     dft8<INV>(v);
-    twiddle_row<8, INV>(v, tw, 32 * l);
+    twiddle_row_w<8, INV>(v, twl(32 * l));
 #pragma unroll
     for (int r = 0; r < 8; r++) p[64 * r] = v[r];
   }
@@ -121,7 +135,7 @@ __device__ __forceinline__ void fft8k_dif(double2* __restrict__ s, const double2
 #pragma unroll
     for (int r = 0; r < 8; r++) v[r] = p[8 * r + (m3 ^ r)];
     dft8<INV>(v);
-    twiddle_row<8, INV>(v, tw, 256 * m3);
+    twiddle_row_w<8, INV>(v, twl(256 * m3));
 #pragma unroll
     for (int r = 0; r < 8; r++) p[8 * r + (m3 ^ r)] = v[r];
   }
@@ -146,7 +160,7 @@ __device__ __forceinline__ void fft8k_dif(double2* __restrict__ s, const double2
 // elementwise consumer.  The transform then ends with the barrier after its last
 // LDS reads, so the caller may write s right away.
 template <bool INV, bool OUT_REGS = false>
-__device__ __forceinline__ void fft8k_dit(double2* __restrict__ s, const double2* __restrict__ tw, int tid,
+__device__ __forceinline__ void fft8k_dit(double2* __restrict__ s, const double2* __restrict__ tw, TwLds twl, int tid,
                                           double2* out = nullptr) {
   __syncthreads();
   {
@@ -170,7 +184,7 @@ __device__ __forceinline__ void fft8k_dit(double2* __restrict__ s, const double2
       double2* p = sub + 64 * (l >> 3);
 #pragma unroll
       for (int r = 0; r < 8; r++) v[r] = p[8 * r + (m3 ^ r)];
-      twiddle_row<8, INV>(v, tw, 256 * m3);
+      twiddle_row_w<8, INV>(v, twl(256 * m3));
       dft8<INV>(v);
 #pragma unroll
       for (int r = 0; r < 8; r++) p[8 * r + (m3 ^ r)] = v[r];
@@ -180,9 +194,9 @@ __device__ __forceinline__ void fft8k_dit(double2* __restrict__ s, const double2
       double2* p = sub + SW(l);
 #pragma unroll
       for (int r = 0; r < 8; r++) v[r] = p[64 * r];
-      twiddle_row<8, INV>(v, tw, 32 * l);
+      twiddle_row_w<8, INV>(v, twl(32 * l));
       dft8<INV>(v);
-      stage1_twiddle<INV>(v, tw, q, l);
+      stage1_twiddle<INV>(v, tw, twl, q, l);
 #pragma unroll
       for (int r = 0; r < 8; r++) p[64 * r] = v[r];
     }

@@ -94,8 +94,10 @@ __device__ __forceinline__ void iir_wave_carries(IIRAux* aux, const double* __re
 
 // FPsync over the sync detector bits: y[n] = b0 (x[n] + x[n-1]) + p y[n-1].
 // bits: bit i = x[16t + i]; xm1 = x[16t - 1].  y[i] = y[16t + i].
+// pl, pt: the table's p^(16 lane), p^(16 t), loaded by the caller (ahead of
+// its global stores: a load issued after them waits for them).
 __device__ __forceinline__ void iir1_bits(uint32_t bits, uint32_t xm1, const double* __restrict__ tab, IIRAux* aux,
-                                          int tid, double* y) {
+                                          int tid, double pl, double pt, double* y) {
   const double b0 = tab[0], p = -tab[2];
   const double* pw = tab + IIR_P1;
   const int lane = tid & 63, w = tid >> 6;
@@ -117,8 +119,8 @@ __device__ __forceinline__ void iir1_bits(uint32_t bits, uint32_t xm1, const dou
   if (lane == 0) st = 0.0;
   if (lane == 63) aux->tot[w][0] = e;
   iir_wave_carries<1>(aux, pw, tid);
-  st = __fma_rn(pw[lane], aux->k[w][0], st);
-  st = __fma_rn(pw[tid], aux->k[16][0], st);
+  st = __fma_rn(pl, aux->k[w][0], st);
+  st = __fma_rn(pt, aux->k[16][0], st);
   prev = xm1 & 1u;
 #pragma unroll
   for (int i = 0; i < IIR_CHUNK; i++) {
@@ -132,8 +134,13 @@ __device__ __forceinline__ void iir1_bits(uint32_t bits, uint32_t xm1, const dou
 // Second-order section y[n] = b0 x[n] + b1 x[n-1] + b2 x[n-2] - a1 y[n-1] - a2 y[n-2]
 // (cf = b0 b1 b2 a1 a2; pw = its C^(16 s) table).  x[i] = x[16t + i],
 // xm1, xm2 = x[16t - 1], x[16t - 2] (circular).  y[i] = y[16t + i].
+// ml, mt: C^(16 lane), C^(16 t) from the table, loaded by the caller.
+__device__ __forceinline__ double4 iir2_pow(const double* __restrict__ pw, int s) {
+  return *reinterpret_cast<const double4*>(pw + 4 * s);
+}
 __device__ __forceinline__ void iir2(const double* x, double xm1, double xm2, const double* __restrict__ cf,
-                                     const double* __restrict__ pw, IIRAux* aux, int tid, double* y) {
+                                     const double* __restrict__ pw, IIRAux* aux, int tid, double4 ml, double4 mt,
+                                     double* y) {
   const double b0 = cf[0], b1 = cf[1], b2 = cf[2], a1 = cf[3], a2 = cf[4];
   const int lane = tid & 63, w = tid >> 6;
   double e0 = 0.0, e1 = 0.0;
@@ -168,8 +175,6 @@ __device__ __forceinline__ void iir2(const double* x, double xm1, double xm2, co
   iir_wave_carries<2>(aux, pw, tid);
   {
     const double K0 = aux->k[w][0], K1 = aux->k[w][1], E0 = aux->k[16][0], E1 = aux->k[16][1];
-    const double4 ml = *reinterpret_cast<const double4*>(pw + 4 * lane);
-    const double4 mt = *reinterpret_cast<const double4*>(pw + 4 * tid);
     s0 = __fma_rn(ml.x, K0, __fma_rn(ml.y, K1, s0));
     s1 = __fma_rn(ml.z, K0, __fma_rn(ml.w, K1, s1));
     s0 = __fma_rn(mt.x, E0, __fma_rn(mt.y, E1, s0));
