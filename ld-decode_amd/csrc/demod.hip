@@ -638,6 +638,8 @@ extern "C" __global__ __launch_bounds__(1024) void ldg_k_audio1(
   const int copylen = (off + (BLOCKLEN - BLOCKCUT) > rd.n_out) ? rd.n_out - off : BLOCKSTEP;
   constexpr double TAU = 6.283185307179586;
   const double2* as = aslice + ((int64_t)slot * MAX_BLOCKS_PER_READ + b) * 2048;
+  __shared__ double s_atan[65];
+  if (tid < 65) s_atan[tid] = c_atan64[tid];   // ordered by the transform's first barrier
   A_[tid] = as[tid];
   A_[1024 + tid] = as[1024 + tid];
   {
@@ -646,7 +648,10 @@ extern "C" __global__ __launch_bounds__(1024) void ldg_k_audio1(
     fft_lds<1024, 512, true>(ga, tw, lt);
     double th[2];
 #pragma unroll
-    for (int e = 0; e < 2; e++) { const double2 z = ga[lt + 512 * e]; th[e] = atan2(z.y, z.x); }
+    for (int e = 0; e < 2; e++) {
+      const double2 z = ga[lt + 512 * e];
+      th[e] = kFastAtan2 ? fast_atan2(z.y, z.x, s_atan) : atan2(z.y, z.x);
+    }
     __syncthreads();
     double* gth = reinterpret_cast<double*>(s_a) + (g ? 1024 : 0);     // plain (unswizzled) phase scratch
 #pragma unroll
@@ -682,8 +687,11 @@ extern "C" __global__ __launch_bounds__(1024) void ldg_k_audio2(
     const double* __restrict__ audio1, int64_t aread_stride, int64_t achan_stride,
     double* __restrict__ audio2, int64_t a2read_stride, int64_t a2chan_stride, const int32_t* __restrict__ status) {
   __shared__ double2 s_x[M];
+  __shared__ double2 s_tw[TW_LDS_N];
   const CBuf X_{s_x};
   const int tid = threadIdx.x;
+  s_tw[tw_lds_pos(tid)] = tw[2 * tid];
+  const TwLds twl{s_tw};
   const int ch = blockIdx.x & 1;
   const int j = (blockIdx.x >> 1) & 7;
   const int slot = smap[blockIdx.x >> 4];
@@ -702,14 +710,14 @@ extern "C" __global__ __launch_bounds__(1024) void ldg_k_audio2(
     const int m = tid + T * q;
     X_[m] = make_double2(src[2 * m], src[2 * m + 1]);
   }
-  fft_lds<M, T, false>(X_, tw, tid);
+  fft8k_dif<false>(s_x, tw, twl, tid);     // digit-reversed out (fft8k.hpp)
   // X[k] for k in [0, 2048]
   double2 xa, xb, xc = make_double2(0, 0);
   {
     const int k1 = tid, k2 = tid + 1024;
-    xa = rsplit(X_[k1], X_[(M - k1) & (M - 1)], tw[k1]);
-    xb = rsplit(X_[k2], X_[M - k2], tw[k2]);
-    if (tid == 0) xc = rsplit(X_[2048], X_[M - 2048], tw[2048]);
+    xa = rsplit(X_[dr_pos(k1)], X_[dr_pos((M - k1) & (M - 1))], tw[k1]);
+    xb = rsplit(X_[dr_pos(k2)], X_[dr_pos(M - k2)], tw[k2]);
+    if (tid == 0) xc = rsplit(X_[dr_pos(2048)], X_[dr_pos(M - 2048)], tw[2048]);
   }
   __syncthreads();
   // S[j] = X[j] (j < 2048); S[j] = conj(X[4096 - j]) (j >= 2048); times lpf2
