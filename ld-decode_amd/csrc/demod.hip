@@ -482,7 +482,7 @@ extern "C" __global__ __launch_bounds__(1024) void ldg_k_demod(
   //  d. demod_burst (and PAL demod_pilot): FVideoBurst = FVideo * Fburst
   //     (:204-209), so the periodic recurrence of Fburst over demod (iir.hpp).
   const double inv = 1.0 / (double)M;
-  double pl1, pt1;
+  double pl1, pt1, p151, p311;
   double2* sx = s_x;                             // chunk layout SWC (iir.hpp) from here on
   {
     merge_pairs(X_, twk, g_05, tid, D);
@@ -494,6 +494,8 @@ extern "C" __global__ __launch_bounds__(1024) void ldg_k_demod(
     // the sync scan's per-lane powers, loaded ahead of this phase's stores
     pl1 = iir[IIR_P1 + (t & 63)];
     pt1 = iir[IIR_P1 + t];
+    p151 = iir[IIR_P1 + scan_d15(t & 63)];
+    p311 = iir[IIR_P1 + scan_d31(t & 63)];
     double* o = vout + (int64_t)CH_05 * vchan_stride;
 #pragma unroll
     for (int q = 0; q < 8; q++) {
@@ -532,7 +534,7 @@ extern "C" __global__ __launch_bounds__(1024) void ldg_k_demod(
     const int t = fresh(tid);
     const uint32_t cur = s_bits[(t + 2) & 1023], prv = (uint32_t)s_bits[(t + 1) & 1023] >> 15;
     double y[IIR_CHUNK];
-    iir1_bits(cur, prv, iir, &s_aux, t, pl1, pt1, y);
+    iir1_bits(cur, prv, iir, &s_aux, t, pl1, pt1, p151, p311, y);
     // sync tiles (common.hpp SyncTile): tile j = outputs [off + 32 j, +32) =
     // block positions [1024 + 32 j, +32) = chunks of threads 64 + 2 j (+1); np.argmax
     // order, the lower half wins ties
@@ -566,7 +568,7 @@ extern "C" __global__ __launch_bounds__(1024) void ldg_k_demod(
   store_chan(sx, vout + (int64_t)CH_SYNC * vchan_stride, tid, copylen);
   __syncthreads();
   STAMP(15);
-  double4 mlb, mtb;
+  double4 mlb, mtb, m15b, m31b;
   {
     merge_pairs(X_, twk, g_video, tid, D);
     STAMP(16);
@@ -576,6 +578,8 @@ extern "C" __global__ __launch_bounds__(1024) void ldg_k_demod(
     const int t = fresh(tid);
     mlb = iir2_pow(iir + IIR_MB, t & 63);     // the burst scan's powers, ahead of the stores
     mtb = iir2_pow(iir + IIR_MB, t);
+    m15b = iir2_pow(iir + IIR_MB, scan_d15(t & 63));
+    m31b = iir2_pow(iir + IIR_MB, scan_d31(t & 63));
     double* o = vout + (int64_t)CH_DEMOD * vchan_stride;
 #pragma unroll
     for (int q = 0; q < 8; q++) {
@@ -598,7 +602,7 @@ extern "C" __global__ __launch_bounds__(1024) void ldg_k_demod(
     }
     const double2 h = sx[SWC((8 * t - 1) & (M - 1))];
     double y[IIR_CHUNK];
-    iir2(x, h.y, h.x, iir + 3, iir + IIR_MB, &s_aux, t, mlb, mtb, y);
+    iir2(x, h.y, h.x, iir + 3, iir + IIR_MB, &s_aux, t, mlb, mtb, m15b, m31b, y);
 #pragma unroll
     for (int c = 0; c < 8; c++) sx[SWC(8 * t + c)] = make_double2(y[2 * c], y[2 * c + 1]);
     __syncthreads();
@@ -606,7 +610,8 @@ extern "C" __global__ __launch_bounds__(1024) void ldg_k_demod(
     if (C.n_chan > 4) {
       // pilot from the same demod samples (still in x); iir2's barriers order
       // the burst stores' LDS reads before the writes below
-      iir2(x, h.y, h.x, iir + 8, iir + IIR_MP, &s_aux, t, iir2_pow(iir + IIR_MP, t & 63), iir2_pow(iir + IIR_MP, t), y);
+      iir2(x, h.y, h.x, iir + 8, iir + IIR_MP, &s_aux, t, iir2_pow(iir + IIR_MP, t & 63), iir2_pow(iir + IIR_MP, t),
+           iir2_pow(iir + IIR_MP, scan_d15(t & 63)), iir2_pow(iir + IIR_MP, scan_d31(t & 63)), y);
 #pragma unroll
       for (int c = 0; c < 8; c++) sx[SWC(8 * t + c)] = make_double2(y[2 * c], y[2 * c + 1]);
       __syncthreads();

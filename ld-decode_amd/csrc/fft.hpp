@@ -2,8 +2,10 @@
 //
 // Data lives in LDS as interleaved complex doubles (one 16-byte double2 per
 // point, ds_read_b128 / ds_write_b128) under an XOR swizzle
-//     slot(i) = i ^ ((i >> 3) & 7)
-// that permutes points inside aligned groups of 8.  Unit-stride reads stay a
+//     slot(i) = i ^ ((i >> 3) & 7) ^ ((i >> 3) & 8)
+// that permutes points inside aligned groups of 16 (bits 3-5 into bits 0-2,
+// bit 6 into bit 3: the latter keeps fft8k.hpp's strided inner stages free of
+// 2-way conflicts under ds_read_b128's 16-lane groups).  Unit-stride reads stay a
 // permutation of 16 consecutive slots (64 banks, conflict-free for the
 // 4 x 16-lane groups of ds_read_b128), and the stride-8 writes of the first
 // Stockham pass land on 8 distinct 16-byte bank groups (conflict-free for the
@@ -21,7 +23,7 @@ namespace ldg {
 
 constexpr int TW_N = 16384;
 
-__device__ __forceinline__ constexpr int SW(int i) { return i ^ ((i >> 3) & 7); }
+__device__ __forceinline__ constexpr int SW(int i) { return i ^ ((i >> 3) & 7) ^ ((i >> 3) & 8); }
 
 // Swizzled complex buffer in LDS.
 struct CBuf {

@@ -9,7 +9,8 @@
 // of step: one wave's LDS stores overlap another wave's FP64 work.  There are
 // four LDS round trips per point, not five.
 //
-// Layouts (same XOR swizzle as fft.hpp, through SW):
+// Layouts (same XOR swizzle as fft.hpp, through SW; the inner stages address
+// the same physical slots SW(64 a + 8 b + c) = 64 a + 8 (b ^ (a & 1)) + (c ^ b)):
 //   * fft8k_dif: the forward transform.  Natural order in, digit-reversed out:
 //     bin k = q + 16 s + 128 u + 1024 v lands at position dr_pos(k) =
 //     512 q + 64 s + 8 u + v.
@@ -117,33 +118,34 @@ __device__ __forceinline__ void fft8k_dif(double2* __restrict__ s, const double2
   double2* sub = s + 512 * q;
   double2 v[8];
   {
-    // stage 2: radix 8 over stride 64 inside the sub-array
-    double2* p = sub + SW(l);
+    // stage 2: radix 8 over stride 64 inside the sub-array (slot of 64 r + l:
+    // 64 r + SW(l) with bit 3 flipped for odd r)
+    const int swl = SW(l);
 #pragma unroll
-    for (int r = 0; r < 8; r++) v[r] = p[64 * r];
+    for (int r = 0; r < 8; r++) v[r] = sub[64 * r + (swl ^ ((r & 1) << 3))];
     stage1_twiddle<INV>(v, tw, twl, q, l);
     dft8<INV>(v);
     twiddle_row_w<8, INV>(v, twl(32 * l));
 #pragma unroll
-    for (int r = 0; r < 8; r++) p[64 * r] = v[r];
+    for (int r = 0; r < 8; r++) sub[64 * r + (swl ^ ((r & 1) << 3))] = v[r];
   }
   wave_lds_sync();
   {
-    // stage 3: radix 8 over stride 8 inside each 64-point block
-    const int m3 = l & 7;
+    // stage 3: radix 8 over stride 8 inside each 64-point block (a = l >> 3)
+    const int m3 = l & 7, a1 = (l >> 3) & 1;
     double2* p = sub + 64 * (l >> 3);
 #pragma unroll
-    for (int r = 0; r < 8; r++) v[r] = p[8 * r + (m3 ^ r)];
+    for (int r = 0; r < 8; r++) v[r] = p[8 * (r ^ a1) + (m3 ^ r)];
     dft8<INV>(v);
     twiddle_row_w<8, INV>(v, twl(256 * m3));
 #pragma unroll
-    for (int r = 0; r < 8; r++) p[8 * r + (m3 ^ r)] = v[r];
+    for (int r = 0; r < 8; r++) p[8 * (r ^ a1) + (m3 ^ r)] = v[r];
   }
   wave_lds_sync();
   {
     // stage 4: radix 8 on each 8 consecutive points
     const int x = l & 7;
-    double2* p = sub + 8 * l;
+    double2* p = sub + 8 * (l ^ ((l >> 3) & 1));
 #pragma unroll
     for (int r = 0; r < 8; r++) v[r] = p[r ^ x];
     dft8<INV>(v);
@@ -171,7 +173,7 @@ __device__ __forceinline__ void fft8k_dit(double2* __restrict__ s, const double2
     double2 v[8];
     {
       const int x = l & 7;
-      double2* p = sub + 8 * l;
+      double2* p = sub + 8 * (l ^ ((l >> 3) & 1));
 #pragma unroll
       for (int r = 0; r < 8; r++) v[r] = p[r ^ x];
       dft8<INV>(v);
@@ -180,25 +182,25 @@ __device__ __forceinline__ void fft8k_dit(double2* __restrict__ s, const double2
     }
     wave_lds_sync();
     {
-      const int m3 = l & 7;
+      const int m3 = l & 7, a1 = (l >> 3) & 1;
       double2* p = sub + 64 * (l >> 3);
 #pragma unroll
-      for (int r = 0; r < 8; r++) v[r] = p[8 * r + (m3 ^ r)];
+      for (int r = 0; r < 8; r++) v[r] = p[8 * (r ^ a1) + (m3 ^ r)];
       twiddle_row_w<8, INV>(v, twl(256 * m3));
       dft8<INV>(v);
 #pragma unroll
-      for (int r = 0; r < 8; r++) p[8 * r + (m3 ^ r)] = v[r];
+      for (int r = 0; r < 8; r++) p[8 * (r ^ a1) + (m3 ^ r)] = v[r];
     }
     wave_lds_sync();
     {
-      double2* p = sub + SW(l);
+      const int swl = SW(l);
 #pragma unroll
-      for (int r = 0; r < 8; r++) v[r] = p[64 * r];
+      for (int r = 0; r < 8; r++) v[r] = sub[64 * r + (swl ^ ((r & 1) << 3))];
       twiddle_row_w<8, INV>(v, twl(32 * l));
       dft8<INV>(v);
       stage1_twiddle<INV>(v, tw, twl, q, l);
 #pragma unroll
-      for (int r = 0; r < 8; r++) p[64 * r] = v[r];
+      for (int r = 0; r < 8; r++) sub[64 * r + (swl ^ ((r & 1) << 3))] = v[r];
     }
   }
   __syncthreads();
