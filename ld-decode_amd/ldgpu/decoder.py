@@ -268,8 +268,10 @@ class GPUDecoder:
             i += 1
         return None if best is None else self.hints[best]
 
-    def _plan(self, nextsample, mtf, last_framenr, isclv, firstframe, want, hist):
-        """Simulate the replay from a frame checkpoint; return up to `want` undecoded keys it will need."""
+    def _plan(self, nextsample, mtf, last_framenr, isclv, firstframe, want, hist, frames_left=None):
+        """Simulate the replay from a frame checkpoint; return up to `want` undecoded keys it will need.
+        frames_left: the decode stops after this many more frames (lddecode.py:49,88 num_frames),
+        so reads past that frame are never needed."""
         new, seen, chain = [], set(), []
         starts = list(hist)
         # the replay stops once the last read's fd.tell() + 1.05 frames passes the
@@ -280,7 +282,8 @@ class GPUDecoder:
         sample, cur_mtf, fr = int(nextsample), mtf, last_framenr
         prev_top = None
         steps = 0
-        while len(new) < want and steps < 8 * want:
+        nframes = 0
+        while len(new) < want and steps < 8 * want and (frames_left is None or nframes < frames_left):
             fieldcount = 0
             last = None
             while fieldcount < 2 and steps < 8 * want:
@@ -344,6 +347,7 @@ class GPUDecoder:
                     self.trace.append((key, hit is not None, istop, fnr, fieldcount, nxt, hk))
             if last is None:
                 break
+            nframes += 1
             fnr, clv = last
             isclv = clv
             if fnr is not None:
@@ -654,7 +658,7 @@ class GPUDecoder:
                 want = self.batch if steady else min(self.batch, 8 if self._hint_keys else 4)
                 tp = time.perf_counter()
                 plan, chain = self._plan(nextsample, self.mtf_level, self.last_framenr, self.last_isclv, done == 0,
-                                         want, hist)
+                                         want, hist, frames_left=num_frames - done + 2)
                 self.stats['plan_s'] = self.stats.get('plan_s', 0.0) + time.perf_counter() - tp
                 if not plan:
                     break
