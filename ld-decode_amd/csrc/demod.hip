@@ -141,6 +141,13 @@ __device__ __forceinline__ bool pair_live(int tid, int c) { return c < 4 || tid 
 __device__ __forceinline__ double2 tw_mirror(double2 w) { return make_double2(-w.x, w.y); }
 
 // Timing probe only (-DLDG_PROBE_NOSTORE): the channel stores are skipped, results are garbage.
+// Timing probes only (-DLDG_PROBE=bits): 1 no atan2, 2 no video transform,
+// 4 no IIR scans, 8 no raw transform.  Results are garbage.
+#ifdef LDG_PROBE
+constexpr int kProbe = LDG_PROBE;
+#else
+constexpr int kProbe = 0;
+#endif
 #ifdef LDG_PROBE_NOSTORE
 constexpr bool kProbeNoStore = true;
 #else
@@ -150,11 +157,20 @@ constexpr bool kProbeNoStore = false;
 // Store the pair of samples 2m, 2m+1 of a channel (o indexed by block position)
 // if kept ([BLOCKCUT, BLOCKCUT + copylen)); the wave-uniform test keeps the
 // common case (a wave's 64 pairs all kept or all dropped) branch-free.
+// A channel's 16-byte store, non-temporal ("nt": streamed, the lines still land
+// in L2 for the field kernels; -1.9% demod time against plain stores in an
+// interleaved A/B, "sc1" +13%).  Inline asm: nothing in the kernel reads these
+// addresses back, so the compiler's wait counting need not see them.
+__device__ __forceinline__ void st_pair(double* a, double2 z) {
+  typedef double v2d __attribute__((ext_vector_type(2)));
+  const v2d zv = {z.x, z.y};
+  asm volatile("global_store_dwordx4 %0, %1, off nt" ::"v"(a), "v"(zv) : "memory");
+}
 __device__ __forceinline__ void store_pair(double* o, int m, double2 z, int copylen) {
   const int p = 2 * m;
   const int pw0 = 2 * (m & ~63);
   if (pw0 >= BLOCKCUT && pw0 + 127 < BLOCKCUT + copylen) {
-    *reinterpret_cast<double2*>(o + p) = z;
+    st_pair(o + p, z);
   } else if (pw0 + 127 >= BLOCKCUT && pw0 < BLOCKCUT + copylen) {
     const bool in0 = p >= BLOCKCUT && p < BLOCKCUT + copylen;
     const bool in1 = p + 1 >= BLOCKCUT && p + 1 < BLOCKCUT + copylen;
@@ -357,7 +373,8 @@ extern "C" __global__ __launch_bounds__(1024) void ldg_k_demod(
     }
   }
   STAMP(1);
-  fft8k_dif<false>(s_x, tw, twl, tid);
+  if (!(kProbe & 8)) fft8k_dif<false>(s_x, tw, twl, tid);
+  else __syncthreads();
   STAMP(2);
 
   // ---- 2. analytic-signal spectra and the audio carrier slices ---------------
@@ -436,7 +453,7 @@ extern "C" __global__ __launch_bounds__(1024) void ldg_k_demod(
 #pragma unroll
     for (int q = 0; q < 8; q++) {
       const double2 z = zr[q];
-      const double a = kFastAtan2 ? fast_atan2(z.y, z.x, s_atan) : atan2(z.y, z.x);
+      const double a = (kProbe & 1) ? z.y * 0.5 + z.x : kFastAtan2 ? fast_atan2(z.y, z.x, s_atan) : atan2(z.y, z.x);
       if (h) tho[q] = a;
       else the[q] = a;
     }
@@ -509,7 +526,7 @@ extern "C" __global__ __launch_bounds__(1024) void ldg_k_demod(
         // the wave's 64 pairs are all kept or all dropped except at the block ends
         const int pw0 = (2 * (m & ~63) - BLOCKCUT_END) & (BLOCKLEN - 1);
         if (pw0 >= BLOCKCUT && pw0 + 127 < BLOCKCUT + copylen) {
-          *reinterpret_cast<double2*>(o + p0) = make_double2(v0, v1);
+          st_pair(o + p0, make_double2(v0, v1));
         } else {
           if (in0 && in1) *reinterpret_cast<double2*>(o + p0) = make_double2(v0, v1);
           else if (in0) o[p0] = v0;
@@ -534,7 +551,8 @@ extern "C" __global__ __launch_bounds__(1024) void ldg_k_demod(
     const int t = fresh(tid);
     const uint32_t cur = s_bits[(t + 2) & 1023], prv = (uint32_t)s_bits[(t + 1) & 1023] >> 15;
     double y[IIR_CHUNK];
-    iir1_bits(cur, prv, iir, &s_aux, t, pl1, pt1, p151, p311, y);
+    if (!(kProbe & 4)) iir1_bits(cur, prv, iir, &s_aux, t, pl1, pt1, p151, p311, y);
+    else for (int i = 0; i < IIR_CHUNK; i++) y[i] = (double)((cur >> i) & 1) * pl1;
     // sync tiles (common.hpp SyncTile): tile j = outputs [off + 32 j, +32) =
     // block positions [1024 + 32 j, +32) = chunks of threads 64 + 2 j (+1); np.argmax
     // order, the lower half wins ties
@@ -573,7 +591,8 @@ extern "C" __global__ __launch_bounds__(1024) void ldg_k_demod(
     merge_pairs(X_, twk, g_video, tid, D);
     STAMP(16);
     double2 zr[8];
-    fft8k_dit<true, true>(s_x, tw, twl, tid, zr);
+    if (!(kProbe & 2)) fft8k_dit<true, true>(s_x, tw, twl, tid, zr);
+    else { __syncthreads(); for (int q = 0; q < 8; q++) zr[q] = s_x[tid + 1024 * q]; __syncthreads(); }
     STAMP(17);
     const int t = fresh(tid);
     mlb = iir2_pow(iir + IIR_MB, t & 63);     // the burst scan's powers, ahead of the stores
@@ -602,7 +621,8 @@ extern "C" __global__ __launch_bounds__(1024) void ldg_k_demod(
     }
     const double2 h = sx[SWC((8 * t - 1) & (M - 1))];
     double y[IIR_CHUNK];
-    iir2(x, h.y, h.x, iir + 3, iir + IIR_MB, &s_aux, t, mlb, mtb, m15b, m31b, y);
+    if (!(kProbe & 4)) iir2(x, h.y, h.x, iir + 3, iir + IIR_MB, &s_aux, t, mlb, mtb, m15b, m31b, y);
+    else for (int i = 0; i < IIR_CHUNK; i++) y[i] = x[i] * mlb.x + h.x;
 #pragma unroll
     for (int c = 0; c < 8; c++) sx[SWC(8 * t + c)] = make_double2(y[2 * c], y[2 * c + 1]);
     __syncthreads();
