@@ -32,6 +32,11 @@ constexpr CTab make_ctab() {
   return t;
 }
 __constant__ CTab g_ctab = make_ctab();        // Thomas c'_t for diag 4 / off-diag 1 (fixed point from t=14)
+constexpr double kCtInf = make_ctab().v[16];    // c'_t for t >= 16
+// Spline evaluation M/6 terms as products with 1/6 (the reference's splev is
+// FITPACK's B-spline evaluation, so no formula reproduces its rounding; the
+// .tbc values agree within the +-1 LSB bar either way)
+constexpr double kSixth = 1.0 / 6.0;
 __device__ __forceinline__ double ctab(int64_t t) { return g_ctab.v[t < 16 ? t : 16]; }
 
 // Truncation margin of a windowed spline solve (the burst pass needs 40 of a
@@ -65,37 +70,50 @@ struct SplineLDS {
   double ys[CAP];
   double ms[CAP];
   double ct[17];
-  double wa[NT / 64], wb[NT / 64];
-  double carry[NT];
+  double ra[NT / 16], rb[NT / 16];
   double m1, mn1;
 };
 
-// Inclusive scan of affine maps x -> A x + B over the workgroup's threads in
-// order (suffix: in reverse order); returns the carry-in of this thread's
-// chunk, i.e. the composition of all earlier (later) chunks applied to 0.
-template <int NT, class SL>
-__device__ __forceinline__ double block_affine_carry(double A, double B, bool suffix, int tid, SL& S) {
-  const int lane = tid & 63, wv = tid >> 6;
-  constexpr int NW = NT / 64;
-  for (int o = 1; o < 64; o <<= 1) {
-    const double pa = suffix ? __shfl_down(A, o) : __shfl_up(A, o);
-    const double pb = suffix ? __shfl_down(B, o) : __shfl_up(B, o);
-    if (suffix ? (lane + o < 64) : (lane >= o)) { B = A * pb + B; A = A * pa; }
-  }
-  if constexpr (NW > 1) {
-    if (lane == (suffix ? 0 : 63)) { S.wa[wv] = A; S.wb[wv] = B; }
-    __syncthreads();
-    if (suffix) {
-      for (int w = wv + 1; w < NW; w++) { B = A * S.wb[w] + B; A = A * S.wa[w]; }
-    } else {
-      for (int w = wv - 1; w >= 0; w--) { B = A * S.wb[w] + B; A = A * S.wa[w]; }
-    }
-  }
-  S.carry[tid] = B;
+// Composition of affine maps x -> A x + B over the workgroup's threads in order
+// (SUFFIX: in reverse order); returns the carry-in of this thread's chunk, i.e.
+// the composition of all earlier (later) chunks applied to 0.  Inside each row
+// of 16 lanes a Kogge-Stone scan by DPP row shifts (no LDS round trip), the
+// row totals through LDS, then each thread folds the rows before (after) its own.
+template <int CTRL>
+__device__ __forceinline__ double dpp_f64_or(double x, double ident) {
+  const int lo = __builtin_amdgcn_update_dpp(__double2loint(ident), __double2loint(x), CTRL, 0xf, 0xf, false);
+  const int hi = __builtin_amdgcn_update_dpp(__double2hiint(ident), __double2hiint(x), CTRL, 0xf, 0xf, false);
+  return __hiloint2double(hi, lo);
+}
+template <bool SUFFIX, int CTRL>
+__device__ __forceinline__ void affine_row_step(double& A, double& B) {
+  const double pa = dpp_f64_or<CTRL>(A, 1.0), pb = dpp_f64_or<CTRL>(B, 0.0);
+  B = A * pb + B;
+  A = A * pa;
+}
+template <int NT, bool SUFFIX, class SL>
+__device__ __forceinline__ double block_affine_carry(double A, double B, int tid, SL& S) {
+  static_assert(NT / 16 <= 16, "row totals");
+  constexpr int NR = NT / 16;
+  const int row = tid >> 4, li = tid & 15;
+  // inclusive within the row: prefix from lanes below (row_shr), suffix from above (row_shl)
+  affine_row_step<SUFFIX, SUFFIX ? 0x101 : 0x111>(A, B);
+  affine_row_step<SUFFIX, SUFFIX ? 0x102 : 0x112>(A, B);
+  affine_row_step<SUFFIX, SUFFIX ? 0x104 : 0x114>(A, B);
+  affine_row_step<SUFFIX, SUFFIX ? 0x108 : 0x118>(A, B);
+  if (li == (SUFFIX ? 0 : 15)) { S.ra[row] = A; S.rb[row] = B; }
+  // exclusive within the row: the neighbour's inclusive value (identity at the row end)
+  const double exA = dpp_f64_or<SUFFIX ? 0x101 : 0x111>(A, 1.0);
+  const double exB = dpp_f64_or<SUFFIX ? 0x101 : 0x111>(B, 0.0);
   __syncthreads();
-  const double c = suffix ? (tid + 1 < NT ? S.carry[tid + 1] : 0.0) : (tid ? S.carry[tid - 1] : 0.0);
+  double rb = 0.0;
+  if (SUFFIX) {
+    for (int r = NR - 1; r > row; r--) rb = S.ra[r] * rb + S.rb[r];
+  } else {
+    for (int r = 0; r < row; r++) rb = S.ra[r] * rb + S.rb[r];
+  }
   __syncthreads();
-  return c;
+  return exA * rb + exB;
 }
 
 template <int NT, int STK = -1, bool PRELOADED = false, class SL, class Sink>
@@ -173,7 +191,7 @@ __device__ int spline_block(const double* __restrict__ buf, int64_t len, double 
       B = (rr[q] - B) * c;
     }
   }
-  double dprev = block_affine_carry<NT>(A, B, false, tid, S);
+  double dprev = block_affine_carry<NT, false>(A, B, tid, S);
   if constexpr (STK >= 0) KSTAMP(STK, 2);
 #pragma unroll
   for (int q = 0; q < CHMAX; q++) {
@@ -194,7 +212,7 @@ __device__ int spline_block(const double* __restrict__ buf, int64_t len, double 
     }
   }
   if constexpr (STK >= 0) KSTAMP(STK, 3);
-  double Mnext = block_affine_carry<NT>(A, B, true, tid, S);
+  double Mnext = block_affine_carry<NT, true>(A, B, tid, S);
   if constexpr (STK >= 0) KSTAMP(STK, 4);
 #pragma unroll
   for (int q = CHMAX - 1; q >= 0; q--) {
@@ -216,7 +234,8 @@ __device__ int spline_block(const double* __restrict__ buf, int64_t len, double 
     const int k = ival(x);
     const double Mk = ms[k], Mk1 = ms[k + 1], yk = ys[k], yk1 = ys[k + 1];
     const double a = (double)(k + 1) - x, b = x - (double)k;
-    const double v = Mk * a * a * a / 6.0 + Mk1 * b * b * b / 6.0 + (yk - Mk / 6.0) * a + (yk1 - Mk1 / 6.0) * b;
+    const double m6 = Mk * kSixth, m16 = Mk1 * kSixth;
+    const double v = m6 * a * a * a + m16 * b * b * b + (yk - m6) * a + (yk1 - m16) * b;
     sink(o, v);
   }
   if constexpr (STK >= 0) KSTAMP(STK, 6);
@@ -463,8 +482,7 @@ constexpr int FINAL_CHMAX = ((SPL_MAXN + FINAL_NT - 1) / FINAL_NT) | 1;   // row
 struct FinalLDS {
   double ms[SPL_MAXN + 1];
   double ct[17];
-  double wa[FINAL_NT / 64], wb[FINAL_NT / 64];
-  double carry[FINAL_NT];
+  double ra[FINAL_NT / 16], rb[FINAL_NT / 16];
   double m1, mn1;
 };
 extern "C" __global__ __launch_bounds__(FINAL_NT) void ldg_k_final_lines(
@@ -516,7 +534,7 @@ extern "C" __global__ __launch_bounds__(FINAL_NT) void ldg_k_final_lines(
   __syncthreads();
   const double M1 = S.m1, Mn1 = S.mn1;
   const double BL = M1, BR = Mn1;
-  auto ct = [&](int t) { return S.ct[t < 16 ? t : 16]; };
+  auto ct = [&](int t) { return t < 16 ? S.ct[t] : kCtInf; };
   double rr[FINAL_CHMAX], cc[FINAL_CHMAX], dd[FINAL_CHMAX];
 #pragma unroll
   for (int q = 0; q < FINAL_CHMAX; q++) {
@@ -539,7 +557,7 @@ extern "C" __global__ __launch_bounds__(FINAL_NT) void ldg_k_final_lines(
       B = (rr[q] - B) * c;
     }
   }
-  double dprev = block_affine_carry<FINAL_NT>(A, B, false, tid, S);
+  double dprev = block_affine_carry<FINAL_NT, false>(A, B, tid, S);
 #pragma unroll
   for (int q = 0; q < FINAL_CHMAX; q++) {
     if (q < nq) {
@@ -558,7 +576,7 @@ extern "C" __global__ __launch_bounds__(FINAL_NT) void ldg_k_final_lines(
       B = dd[q] - c * B;
     }
   }
-  double Mnext = block_affine_carry<FINAL_NT>(A, B, true, tid, S);
+  double Mnext = block_affine_carry<FINAL_NT, true>(A, B, tid, S);
   double* ms = S.ms;
 #pragma unroll
   for (int q = FINAL_CHMAX - 1; q >= 0; q--) {
@@ -585,6 +603,7 @@ extern "C" __global__ __launch_bounds__(FINAL_NT) void ldg_k_final_lines(
   const double scale_ = pal ? (double)(0xd300 - 0x0100) / (100 - C.vsync_ire)
                             : (double)(0xc800 - 0x0400) / (100 - C.vsync_ire);
   const double base = pal ? 256.0 : 1024.0;
+  const double rhz = 1.0 / C.hz_ire;
   constexpr int NO = (MAX_OUTW + FINAL_NT - 1) / FINAL_NT;
   double yk[NO], yk1[NO];
   int kk[NO];
@@ -609,8 +628,9 @@ extern "C" __global__ __launch_bounds__(FINAL_NT) void ldg_k_final_lines(
     const int k = kk[e];
     const double Mk = ms[k], Mk1 = ms[k + 1];
     const double a = (double)(k + 1) - x, b = x - (double)k;
-    const double v = Mk * a * a * a / 6.0 + Mk1 * b * b * b / 6.0 + (yk[e] - Mk / 6.0) * a + (yk1[e] - Mk1 / 6.0) * b;
-    double red = ((v * wow) - C.ire0) / C.hz_ire;
+    const double m6 = Mk * kSixth, m16 = Mk1 * kSixth;
+    const double v = m6 * a * a * a + m16 * b * b * b + (yk[e] - m6) * a + (yk1[e] - m16) * b;
+    double red = ((v * wow) - C.ire0) * rhz;
     red -= C.vsync_ire;
     double px = (red * scale_) + base;
     if (px != px) px = 0.0;
