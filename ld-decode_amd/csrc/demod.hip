@@ -142,7 +142,9 @@ __device__ __forceinline__ double2 tw_mirror(double2 w) { return make_double2(-w
 
 // Timing probe only (-DLDG_PROBE_NOSTORE): the channel stores are skipped, results are garbage.
 // Timing probes only (-DLDG_PROBE=bits): 1 no atan2, 2 no video transform,
-// 4 no IIR scans, 8 no raw transform.  Results are garbage.
+// 4 no IIR scans, 8 no raw transform, 16 no filter/park phase, 32 no merges,
+// 64 no split of the raw and demod spectra, 128 no filter-table loads in the
+// filter phase, 256 no park stores.  Results are garbage.
 #ifdef LDG_PROBE
 constexpr int kProbe = LDG_PROBE;
 #else
@@ -166,6 +168,9 @@ __device__ __forceinline__ void st_pair(double* a, double2 z) {
   const v2d zv = {z.x, z.y};
   asm volatile("global_store_dwordx4 %0, %1, off nt" ::"v"(a), "v"(zv) : "memory");
 }
+// The odd-half park's stores (read back by LDS-DMA on the same CU): plain
+// stores ("nt" measured +1.5%, "sc0" even).
+__device__ __forceinline__ void st_park(double2* a, double2 z) { *a = z; }
 __device__ __forceinline__ void store_pair(double* o, int m, double2 z, int copylen) {
   const int p = 2 * m;
   const int pw0 = 2 * (m & ~63);
@@ -386,7 +391,8 @@ extern "C" __global__ __launch_bounds__(1024) void ldg_k_demod(
   // in the same order (F[p] = bin dr_nat(p), F[M + p] = bin M + dr_nat(p)).
   {
     Pairs X;
-    split_pairs(X_, twk, tid, X);
+    if (!(kProbe & 64)) split_pairs(X_, twk, tid, X);
+    else for (int c = 0; c < 5; c++) { X.a[c] = X_[tid + 1024 * c]; X.b[c] = X.a[c]; }
     {
       // audio carrier slices (lddecode_core.py:321-328): thread t < 512 takes
       // bin k = a0 + t into slot j = t; thread t >= 512 the mirrored bin
@@ -408,18 +414,19 @@ extern "C" __global__ __launch_bounds__(1024) void ldg_k_demod(
     const int t = fresh(tid);
 #pragma unroll
     for (int c = 0; c < 5; c++) {
-      if (!pair_live(t, c)) continue;
+      if (!pair_live(t, c) || (kProbe & 16)) continue;
       const Slot sl = slot_of(t, c);
+      auto Fv = [&](int i) { return (kProbe & 128) ? make_double2(1.0 + i * 1e-9, 0.5) : F[i]; };
       const double2 wk = twk[sl.p];
-      const double2 yk = cmul(X.a[c], F[sl.p]);
-      const double2 yk2 = cmul(conj2(X.b[c]), F[M + sl.p]);
+      const double2 yk = cmul(X.a[c], Fv(sl.p));
+      const double2 yk2 = cmul(conj2(X.b[c]), Fv(M + sl.p));
       X_[sl.p] = cadd(yk, yk2);
-      park[SW(sl.p)] = cmulc(csub(yk, yk2), wk);
+      if (!(kProbe & 256)) st_park(park + SW(sl.p), cmulc(csub(yk, yk2), wk));
       if (sl.pp != sl.p) {
-        const double2 ykp = cmul(X.b[c], F[sl.pp]);
-        const double2 ykp2 = cmul(conj2(X.a[c]), F[M + sl.pp]);
+        const double2 ykp = cmul(X.b[c], Fv(sl.pp));
+        const double2 ykp2 = cmul(conj2(X.a[c]), Fv(M + sl.pp));
         X_[sl.pp] = cadd(ykp, ykp2);
-        park[SW(sl.pp)] = cmulc(csub(ykp, ykp2), tw_mirror(wk));
+        if (!(kProbe & 256)) st_park(park + SW(sl.pp), cmulc(csub(ykp, ykp2), tw_mirror(wk)));
       }
     }
   }
@@ -485,7 +492,8 @@ extern "C" __global__ __launch_bounds__(1024) void ldg_k_demod(
   fft8k_dif<false>(s_x, tw, twl, tid);
   STAMP(10);
   Pairs D;
-  split_pairs(X_, twk, tid, D);
+  if (!(kProbe & 64)) split_pairs(X_, twk, tid, D);
+  else for (int c = 0; c < 5; c++) { D.a[c] = X_[tid + 1024 * c]; D.b[c] = D.a[c]; }
   __syncthreads();
   STAMP(11);
 
@@ -502,7 +510,7 @@ extern "C" __global__ __launch_bounds__(1024) void ldg_k_demod(
   double pl1, pt1, p151, p311;
   double2* sx = s_x;                             // chunk layout SWC (iir.hpp) from here on
   {
-    merge_pairs(X_, twk, g_05, tid, D);
+    if (!(kProbe & 32)) merge_pairs(X_, twk, g_05, tid, D);
     STAMP(12);
     double2 zr[8];                               // outputs at natural positions t + T q
     fft8k_dit<true, true>(s_x, tw, twl, tid, zr);
@@ -588,7 +596,7 @@ extern "C" __global__ __launch_bounds__(1024) void ldg_k_demod(
   STAMP(15);
   double4 mlb, mtb, m15b, m31b;
   {
-    merge_pairs(X_, twk, g_video, tid, D);
+    if (!(kProbe & 32)) merge_pairs(X_, twk, g_video, tid, D);
     STAMP(16);
     double2 zr[8];
     if (!(kProbe & 2)) fft8k_dit<true, true>(s_x, tw, twl, tid, zr);
