@@ -66,6 +66,8 @@ struct SysConst {
   double audio_lfreq, audio_rfreq;
   double line_period;             // us
   double fsc_mhz;
+  double sy_b0, sy_p;             // FPsync recurrence (iir.hpp): b0, p = -a1
+  double bu_b0, bu_b1, bu_b2, bu_a1, bu_a2;   // Fburst recurrence
   int32_t system;                 // 0 NTSC, 1 PAL
   int32_t linelen;                // rf.linelen (2542 / 2560)
   int32_t outlinelen;             // 910 / 1135

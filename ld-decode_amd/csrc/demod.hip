@@ -13,11 +13,13 @@
 // Per block, 8192-point FFTs: raw R2C, analytic even, analytic odd, demod R2C,
 // C2R 0.5 MHz, C2R video = 6 (NTSC and PAL).  The sync, burst and pilot
 // channels, whose filters are sampled butter(1) designs, are their periodic
-// recurrences in the time domain (iir.hpp).
+// recurrences in the time domain (iir.hpp); sync and burst are stored compact,
+// as per-chunk states the field kernels expand (chan.hpp).
 #include <hip/hip_runtime.h>
 #include "common.hpp"
 #include "fft8k.hpp"
 #include "iir.hpp"
+#include "chan.hpp"
 
 using namespace ldg;
 
@@ -312,6 +314,7 @@ extern "C" __global__ __launch_bounds__(1024) void ldg_k_demod(
     double* __restrict__ video, int64_t vread_stride, int64_t vchan_stride,
     double* __restrict__ audio1, int64_t aread_stride, int64_t achan_stride, int32_t* __restrict__ status,
     double2* __restrict__ ospill, SyncTile* __restrict__ stiles, double2* __restrict__ aslice,
+    double* __restrict__ sst, uint32_t* __restrict__ sbits, double4* __restrict__ bst,
     unsigned long long* __restrict__ span) {
   __shared__ double2 s_x[M];          // 128 KiB: the 8192-point transforms
   __shared__ uint16_t s_bits[BLOCKLEN / 16];   // sync detector bits
@@ -559,8 +562,15 @@ extern "C" __global__ __launch_bounds__(1024) void ldg_k_demod(
     const int t = fresh(tid);
     const uint32_t cur = s_bits[(t + 2) & 1023], prv = (uint32_t)s_bits[(t + 1) & 1023] >> 15;
     double y[IIR_CHUNK];
-    if (!(kProbe & 4)) iir1_bits(cur, prv, iir, &s_aux, t, pl1, pt1, p151, p311, y);
+    double st_in = 0.0;
+    if (!(kProbe & 4)) iir1_bits(cur, prv, iir, &s_aux, t, pl1, pt1, p151, p311, y, &st_in);
     else for (int i = 0; i < IIR_CHUNK; i++) y[i] = (double)((cur >> i) & 1) * pl1;
+    // the compact channel (chan.hpp): the kept chunks' entering states and bits
+    if (16 * t >= BLOCKCUT && 16 * t < BLOCKCUT + copylen) {
+      const int64_t g = (int64_t)slot * CHUNKS_PER_SLOT + (off >> 4) + (t - BLOCKCUT / 16);
+      sst[g] = st_in;
+      sbits[g] = cur | (prv << 16);
+    }
     // sync tiles (common.hpp SyncTile): tile j = outputs [off + 32 j, +32) =
     // block positions [1024 + 32 j, +32) = chunks of threads 64 + 2 j (+1); np.argmax
     // order, the lower half wins ties
@@ -587,12 +597,7 @@ extern "C" __global__ __launch_bounds__(1024) void ldg_k_demod(
         stiles[(int64_t)slot * STILE_PER_SLOT + (n0 >> 5)] = tt;
       }
     }
-#pragma unroll
-    for (int c = 0; c < 8; c++) sx[SWC(8 * t + c)] = make_double2(y[2 * c], y[2 * c + 1]);
   }
-  __syncthreads();
-  store_chan(sx, vout + (int64_t)CH_SYNC * vchan_stride, tid, copylen);
-  __syncthreads();
   STAMP(15);
   double4 mlb, mtb, m15b, m31b;
   {
@@ -629,17 +634,19 @@ extern "C" __global__ __launch_bounds__(1024) void ldg_k_demod(
     }
     const double2 h = sx[SWC((8 * t - 1) & (M - 1))];
     double y[IIR_CHUNK];
-    if (!(kProbe & 4)) iir2(x, h.y, h.x, iir + 3, iir + IIR_MB, &s_aux, t, mlb, mtb, m15b, m31b, y);
-    else for (int i = 0; i < IIR_CHUNK; i++) y[i] = x[i] * mlb.x + h.x;
-#pragma unroll
-    for (int c = 0; c < 8; c++) sx[SWC(8 * t + c)] = make_double2(y[2 * c], y[2 * c + 1]);
-    __syncthreads();
-    store_chan(sx, vout + (int64_t)CH_BURST * vchan_stride, t, copylen);
+    double2 s_in = make_double2(0.0, 0.0);
+    if (!(kProbe & 4)) iir2(x, h.y, h.x, iir + 3, iir + IIR_MB, &s_aux, t, mlb, mtb, m15b, m31b, y, &s_in);
+    // the compact burst channel (chan.hpp): the kept chunks' entering states
+    if (16 * t >= BLOCKCUT && 16 * t < BLOCKCUT + copylen) {
+      const int64_t g = (int64_t)slot * CHUNKS_PER_SLOT + (off >> 4) + (t - BLOCKCUT / 16);
+      bst[g] = make_double4(s_in.x, s_in.y, h.y, h.x);
+    }
     if (C.n_chan > 4) {
-      // pilot from the same demod samples (still in x); iir2's barriers order
-      // the burst stores' LDS reads before the writes below
+      // PAL pilot from the same demod samples (still in x); iir2's barriers order
+      // every thread's reads of sx above before the writes below
+      double2 p_in;
       iir2(x, h.y, h.x, iir + 8, iir + IIR_MP, &s_aux, t, iir2_pow(iir + IIR_MP, t & 63), iir2_pow(iir + IIR_MP, t),
-           iir2_pow(iir + IIR_MP, scan_d15(t & 63)), iir2_pow(iir + IIR_MP, scan_d31(t & 63)), y);
+           iir2_pow(iir + IIR_MP, scan_d15(t & 63)), iir2_pow(iir + IIR_MP, scan_d31(t & 63)), y, &p_in);
 #pragma unroll
       for (int c = 0; c < 8; c++) sx[SWC(8 * t + c)] = make_double2(y[2 * c], y[2 * c + 1]);
       __syncthreads();

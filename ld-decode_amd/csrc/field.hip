@@ -15,6 +15,7 @@
 #include "common.hpp"
 #include "field_rec.hpp"
 #include "pyops.hpp"
+#include "chan.hpp"
 
 using namespace ldg;
 
@@ -47,7 +48,8 @@ struct SyncView {
 // maximum; the first NaN wins), one wave: 20 coalesced loads per lane issued
 // back to back, then a cross-lane reduction.  Window <= 1280 samples.
 constexpr int ARGMAX_PER = 20;
-__device__ inline void wave_argmax(const double* __restrict__ ds, int64_t i, int64_t wend, int lane, double& best,
+template <class Src>
+__device__ inline void wave_argmax(const Src& ds, int64_t i, int64_t wend, int lane, double& best,
                                    int64_t& bidx) {
   double vv[ARGMAX_PER];
 #pragma unroll
@@ -69,7 +71,8 @@ __device__ inline void wave_argmax(const double* __restrict__ ds, int64_t i, int
 
 // wave_argmax from the sync tiles: whole tiles inside [i, wend) plus the raw
 // samples of the two ragged ends (one load per lane each instead of 20).
-__device__ inline void tile_argmax(const double* __restrict__ ds, const SyncTile* __restrict__ tiles, int64_t i,
+template <class Src>
+__device__ inline void tile_argmax(const Src& ds, const SyncTile* __restrict__ tiles, int64_t i,
                                    int64_t wend, int lane, double& best, int64_t& bidx) {
   const int64_t t0 = (i + 31) >> 5, t1 = wend >> 5;         // whole tiles [t0, t1)
   if (t0 >= t1) { wave_argmax(ds, i, wend, lane, best, bidx); return; }
@@ -132,7 +135,8 @@ extern "C" __global__ __launch_bounds__(64) void ldg_k_sync_walk(
     const int32_t* __restrict__ smap, const ReadDesc* __restrict__ reads, const double* __restrict__ video,
     int64_t vread_stride, int64_t vchan_stride, SysConst C, const int32_t* __restrict__ status,
     int32_t* __restrict__ node_pos, int32_t* __restrict__ node_pk, double* __restrict__ node_lv,
-    int32_t* __restrict__ node_n, const SyncTile* __restrict__ stiles) {
+    int32_t* __restrict__ node_n, const SyncTile* __restrict__ stiles, const double* __restrict__ sst,
+    const uint32_t* __restrict__ sbits) {
   prio_latency();
 
   const int lane = threadIdx.x;
@@ -145,7 +149,7 @@ extern "C" __global__ __launch_bounds__(64) void ldg_k_sync_walk(
   }
   const ReadDesc rd = reads[slot];
   const WalkGeom G(rd.n_out, C.linelen);
-  const double* ds = video + (int64_t)slot * vread_stride + (int64_t)CH_SYNC * vchan_stride;
+  const SyncSrc ds(sst, sbits, slot, C);
   const SyncTile* tl = stiles + (int64_t)slot * STILE_PER_SLOT;
   int64_t i = (int64_t)k * G.seg;
   int64_t e = (k == SEG_K - 1) ? G.stop : (int64_t)(k + 1) * G.seg + G.ov;
@@ -174,7 +178,7 @@ extern "C" __global__ __launch_bounds__(64) void ldg_k_sync(
     int64_t vchan_stride, SysConst C, FieldRec* __restrict__ recs, int32_t* __restrict__ peaks,
     const int32_t* __restrict__ status, const int32_t* __restrict__ node_pos, const int32_t* __restrict__ node_pk,
     const double* __restrict__ node_lv, const int32_t* __restrict__ node_n, const SyncTile* __restrict__ stiles,
-    int nofast) {
+    const double* __restrict__ sst, const uint32_t* __restrict__ sbits, int nofast) {
   prio_latency();
 
   __shared__ int32_t s_npos[SEG_K * SEG_NMAX];
@@ -195,7 +199,7 @@ extern "C" __global__ __launch_bounds__(64) void ldg_k_sync(
     if (lane == 0) { R->status = FS_EOF; R->npeaks = 0; R->nvsync = 0; }
     return;
   }
-  const double* ds = video + (int64_t)slot * vread_stride + (int64_t)CH_SYNC * vchan_stride;
+  const SyncSrc ds(sst, sbits, slot, C);
   const int64_t len = rd.n_out;
   const int linelen = C.linelen;
   const WalkGeom G(len, linelen);
@@ -512,7 +516,7 @@ extern "C" __global__ __launch_bounds__(64) void ldg_k_sync(
 extern "C" __global__ __launch_bounds__(64) void ldg_k_linelocs(
     const int32_t* __restrict__ smap, const double* __restrict__ video, int64_t vread_stride, int64_t vchan_stride, SysConst C,
     FieldRec* __restrict__ recs, const int32_t* __restrict__ peaks, double* __restrict__ lines,
-    int8_t* __restrict__ bad) {
+    int8_t* __restrict__ bad, const double* __restrict__ sst, const uint32_t* __restrict__ sbits) {
   prio_latency();
 
   __shared__ double s_key[LINENUM_SPAN];
@@ -531,7 +535,7 @@ extern "C" __global__ __launch_bounds__(64) void ldg_k_linelocs(
   if (R->status != FS_PENDING) return;
   const int np = R->npeaks;
   const int32_t* pkg = peaks + (int64_t)slot * MAX_PEAKS;
-  const double* ds = video + (int64_t)slot * vread_stride + (int64_t)CH_SYNC * vchan_stride;
+  const SyncSrc ds(sst, sbits, slot, C);
   for (int k = lane; k < LINENUM_SPAN; k += 64) { s_has[k] = 0; s_orig[k] = 0; }
   for (int k = lane; k < np; k += 64) { const int32_t p = pkg[k]; s_pkl[k] = p; s_lv[k] = ds[p]; }
   if (lane == 0) s_flag = 0;

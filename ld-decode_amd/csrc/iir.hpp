@@ -61,6 +61,17 @@ __device__ __forceinline__ double dpp_f64(double x) {
 __device__ __forceinline__ int scan_d15(int lane) { return (lane & 15) + 1; }
 __device__ __forceinline__ int scan_d31(int lane) { return lane >= 32 ? lane - 31 : 0; }
 
+// One step of each recurrence, in the arithmetic the demod's outputs use; the
+// field kernels rebuild sync / burst values from stored chunk states with the
+// same steps (compact channels, chan.hpp), so the values are bit-identical.
+__device__ __forceinline__ double sync_step(double st, uint32_t x, uint32_t prev, double b0, double p) {
+  return __fma_rn(p, st, b0 * (double)(x + prev));
+}
+__device__ __forceinline__ double sos_step(double x, double xa, double xb, double s0, double s1, double b0, double b1,
+                                           double b2, double a1, double a2) {
+  return b0 * x + b1 * xa + b2 * xb - a1 * s0 - a2 * s1;
+}
+
 // LDS scratch of a scan: wave totals and the states entering each wave.
 struct IIRAux {
   double tot[16][2];
@@ -133,8 +144,10 @@ __device__ __forceinline__ void iir_wave_carries(IIRAux* aux, const double* __re
 // pl, pt: the table's p^(16 lane), p^(16 t), loaded by the caller (ahead of
 // its global stores: a load issued after them waits for them).
 // p15, p31: p^(16 scan_d15(lane)), p^(16 scan_d31(lane)), also loaded by the caller.
+// *st_in: the state entering the chunk (y[16t - 1]).
 __device__ __forceinline__ void iir1_bits(uint32_t bits, uint32_t xm1, const double* __restrict__ tab, IIRAux* aux,
-                                          int tid, double pl, double pt, double p15, double p31, double* y) {
+                                          int tid, double pl, double pt, double p15, double p31, double* y,
+                                          double* st_in) {
   const double b0 = tab[0], p = -tab[2];
   const double* pw = tab + IIR_P1;
   const int lane = tid & 63, w = tid >> 6;
@@ -158,11 +171,12 @@ __device__ __forceinline__ void iir1_bits(uint32_t bits, uint32_t xm1, const dou
   iir_wave_carries<1>(aux, pw, tid);
   st = __fma_rn(pl, aux->k[w][0], st);
   st = __fma_rn(pt, aux->k[16][0], st);
+  *st_in = st;
   prev = xm1 & 1u;
 #pragma unroll
   for (int i = 0; i < IIR_CHUNK; i++) {
     const uint32_t x = (bits >> i) & 1u;
-    st = __fma_rn(p, st, b0 * (double)(x + prev));
+    st = sync_step(st, x, prev, b0, p);
     prev = x;
     y[i] = st;
   }
@@ -178,7 +192,7 @@ __device__ __forceinline__ double4 iir2_pow(const double* __restrict__ pw, int s
 // m15, m31: C^(16 scan_d15(lane)), C^(16 scan_d31(lane)).
 __device__ __forceinline__ void iir2(const double* x, double xm1, double xm2, const double* __restrict__ cf,
                                      const double* __restrict__ pw, IIRAux* aux, int tid, double4 ml, double4 mt,
-                                     double4 m15, double4 m31, double* y) {
+                                     double4 m15, double4 m31, double* y, double2* s_in) {
   const double b0 = cf[0], b1 = cf[1], b2 = cf[2], a1 = cf[3], a2 = cf[4];
   const int lane = tid & 63, w = tid >> 6;
   double e0 = 0.0, e1 = 0.0;
@@ -212,11 +226,12 @@ __device__ __forceinline__ void iir2(const double* x, double xm1, double xm2, co
     s0 = __fma_rn(mt.x, E0, __fma_rn(mt.y, E1, s0));
     s1 = __fma_rn(mt.z, E0, __fma_rn(mt.w, E1, s1));
   }
+  *s_in = make_double2(s0, s1);
   {
     double xa = xm1, xb = xm2;
 #pragma unroll
     for (int i = 0; i < IIR_CHUNK; i++) {
-      const double v = b0 * x[i] + b1 * xa + b2 * xb - a1 * s0 - a2 * s1;
+      const double v = sos_step(x[i], xa, xb, s0, s1, b0, b1, b2, a1, a2);
       s1 = s0;
       s0 = v;
       xb = xa;

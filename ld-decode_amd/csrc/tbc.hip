@@ -16,6 +16,7 @@
 #include "common.hpp"
 #include "field_rec.hpp"
 #include "pyops.hpp"
+#include "chan.hpp"
 
 using namespace ldg;
 
@@ -72,6 +73,7 @@ struct SplineLDS {
   double ct[17];
   double ra[NT / 16], rb[NT / 16];
   double m1, mn1;
+  double ye[6];                     // y[0..2], y[n-2..n] (the not-a-knot end rows)
 };
 
 // Composition of affine maps x -> A x + B over the workgroup's threads in order
@@ -116,8 +118,8 @@ __device__ __forceinline__ double block_affine_carry(double A, double B, int tid
   return exA * rb + exB;
 }
 
-template <int NT, int STK = -1, bool PRELOADED = false, class SL, class Sink>
-__device__ int spline_block(const double* __restrict__ buf, int64_t len, double begin, double end, int W, int o_lo,
+template <int NT, int STK = -1, bool PRELOADED = false, class Src, class SL, class Sink>
+__device__ int spline_block(const Src& buf, int64_t len, double begin, double end, int W, int o_lo,
                             int o_hi, int tid, SL& S, Sink&& sink) {
   if constexpr (STK >= 0) KSTAMP(STK, 0);
   if (tid < 17) S.ct[tid] = g_ctab.v[tid];
@@ -125,7 +127,6 @@ __device__ int spline_block(const double* __restrict__ buf, int64_t len, double 
   const int64_t n64 = ie - ib;
   if (ib < 0 || n64 < 6 || n64 >= SPL_MAXN || ib + n64 + 1 > len) return -1;
   const int n = (int)n64;
-  const double* y = buf + ib;
   const double x0 = begin - (double)ib;
   const double span = end - begin;
   const double step = ((span + x0) - x0) / (double)W;
@@ -150,15 +151,14 @@ __device__ int spline_block(const double* __restrict__ buf, int64_t len, double 
       S.mn1 = (6.0 * ((ys[n] - ys[n - 1]) - (ys[n - 1] - ys[n - 2]))) / 6.0;
     }
   } else {
-    for (int j = base + tid; j <= top; j += NT) ys[j] = y[j];
-    if (tid == 0) {
-      S.m1 = (6.0 * ((y[2] - y[1]) - (y[1] - y[0]))) / 6.0;
-      S.mn1 = (6.0 * ((y[n] - y[n - 1]) - (y[n - 1] - y[n - 2]))) / 6.0;
-    }
+    buf.window(ib + base, ib + top, ys + base, tid, NT);   // ys[j] = y[j], j in [base, top]
+    if (tid < 6) S.ye[tid] = buf[ib + (tid < 3 ? tid : n - 5 + tid)];
   }
   __syncthreads();
   if constexpr (STK >= 0) KSTAMP(STK, 1);
-  const double M1 = S.m1, Mn1 = S.mn1;
+  const double* ye = S.ye;
+  const double M1 = PRELOADED ? S.m1 : (6.0 * ((ye[2] - ye[1]) - (ye[1] - ye[0]))) / 6.0;
+  const double Mn1 = PRELOADED ? S.mn1 : (6.0 * ((ye[5] - ye[4]) - (ye[4] - ye[3]))) / 6.0;
   const double BL = (lo == 2) ? M1 : 0.0, BR = (hi == n - 2) ? Mn1 : 0.0;
   const int T = hi - lo + 1;                                  // rows j = lo + t
   int CH = (T + NT - 1) / NT;
@@ -267,7 +267,8 @@ __device__ inline int calczc_s(const double* d, int len, int s, double target, i
 // grid: n_reads * LINE_GROUPS workgroups of 64 threads; lane = line.
 extern "C" __global__ __launch_bounds__(64) void ldg_k_burst_lines(
     const int32_t* __restrict__ smap, const double* __restrict__ video, int64_t vread_stride, int64_t vchan_stride, SysConst C,
-    FieldRec* __restrict__ recs, double* __restrict__ lines, float* __restrict__ blevel, int pass) {
+    FieldRec* __restrict__ recs, double* __restrict__ lines, float* __restrict__ blevel, int pass,
+    const double4* __restrict__ bst) {
   prio_latency();
 
   // window rows for 40 outputs: <= 40 * SPL_MAXN / W + 2 * KTR + 4 < 384
@@ -289,7 +290,8 @@ extern "C" __global__ __launch_bounds__(64) void ldg_k_burst_lines(
     if (lane == 0) { pv0[l] = 0.0; pv1[l] = 0.0; lvl[l] = 0.0f; }
     return;
   }
-  const double* bur = video + (int64_t)slot * vread_stride + (int64_t)CH_BURST * vchan_stride;
+  // demod_burst from the demod channel and the demod's per-chunk states (chan.hpp)
+  const BurstSrc bur(bst, video + (int64_t)slot * vread_stride + (int64_t)CH_DEMOD * vchan_stride, slot, C);
   const double b0 = li[l], b1 = li[l + 1];
   const double wow = (b1 - b0) / (double)C.linelen;
   const int W = C.outlinelen;
