@@ -35,7 +35,10 @@ BYTES_PER_SAMPLE = {0: 1.0, 1: 2.0, 2: 4 / 3, 3: 1.25}
 HBM_PEAK_GBS = 8000.0
 FP64_PEAK_TFLOPS = 78.6                           # MI355X FP64 vector (spec)
 READ_BLOCKS = 66                                  # overlap-save blocks per 1e6-sample field read
-DEMOD_FLOPS_PER_BLOCK = 9 * 5 * 8192 * 13 + 2 * 5 * 1024 * 10
+# the FFT flops the demod executes per block (5 N log2 N): six 8192-point complex transforms
+# (raw R2C, analytic even / odd, demod R2C, C2R 0.5 MHz, C2R video) + two 1024-point audio IFFTs;
+# sync / burst / pilot are time-domain recurrences (iir.hpp) and are not counted
+DEMOD_FLOPS_PER_BLOCK = 6 * 5 * 8192 * 13 + 2 * 5 * 1024 * 10
 
 
 def parse():
@@ -184,7 +187,7 @@ def main():
         except Exception:
             traffic = None
     # secondary bound of the demod kernel: FP64 vector issue (FFT-convention
-    # flops 5 N log2 N: 9 x 8192-point + 2 x 1024-point complex FFTs per block)
+    # flops 5 N log2 N: 6 x 8192-point + 2 x 1024-point complex FFTs per block)
     fp64 = None
     if 'demod' in stats and stats['demod'][0]:
         blocks = reads_timed * READ_BLOCKS
