@@ -17,6 +17,7 @@ Audio offsets (:1289, :484) are a scalar recurrence computed here with the
 reference's own numpy arithmetic; the per-sample audio resampling runs on the
 GPU for all fields of a batch at once.
 """
+import gc
 import math
 import os
 import time
@@ -184,6 +185,7 @@ class GPUDecoder:
         self.period, self.period_samples = P, D          # exact at 40 MSPS: 3 NTSC / 1 PAL frames
         self.field_nom = int(round(self.rf.freq_hz / self.sysp.fps / 2))
         self.trace = None          # diagnostics: planner steps (tools/miss_probe.py)
+        self.boot_wide = os.environ.get('LDG_BOOT_WIDE', '0') == '1'
         self.comb, self.comb_sink = False, None
         self.comb3d = None                 # (core_ire, range_ire): the 3D comb (comb-ntsc -d 3 -F)
         self.pending = []                  # (keys, slots) of the outstanding decode launches, oldest first
@@ -622,17 +624,28 @@ class GPUDecoder:
         for k, v in (init_state or {}).items():        # chain state handed over by a previous shard
             setattr(self, k, v)
         nextsample = start_frame * spf if start_sample is None else start_sample
+        # Python's cyclic collector off for the decode: a full (oldest-generation)
+        # collection over the read cache and hint index stalls the host for
+        # 10-25 ms, during which the GPU runs dry (measured: one such gap per
+        # 60 s decode, ~5% of a 2-step bench).  The loop collects the young
+        # generations itself every few batches, so cyclic garbage stays bounded.
+        gc_on = gc.isenabled()
+        gc.disable()
         try:
             return self._decode_loop(start_frame, num_frames, nextsample, spf, bpf, size, sink, stop_sample,
                                      keep_from, firstframe)
         finally:
-            while self.pending:                 # no launch outlives the call (an exception included)
-                self._launch_wait()
             try:
-                self._emit_pending()
+                while self.pending:             # no launch outlives the call (an exception included)
+                    self._launch_wait()
+                try:
+                    self._emit_pending()
+                finally:
+                    self._out_pending = None
+                    self.ctx.sync()
             finally:
-                self._out_pending = None
-                self.ctx.sync()
+                if gc_on:
+                    gc.enable()
 
     def _decode_loop(self, start_frame, num_frames, nextsample, spf, bpf, size, sink, stop_sample, keep_from,
                      firstframe):
@@ -652,6 +665,10 @@ class GPUDecoder:
             # through the older one's predicted outcomes, so its demod runs on the GPU
             # while the older one's field kernels finish and the host replays.
             steady = len(hist) >= self.period + 2
+            if self.boot_wide and not steady:
+                # P + 2 decoded reads (hints) already locate the next fields exactly and
+                # seed the period extrapolation: go wide before the replay catches up
+                steady = len(self._hint_keys) >= self.period + 2
             depth = self.depth if steady else 1
             launched = 0
             while len(self.pending) < depth:
@@ -695,6 +712,8 @@ class GPUDecoder:
                 frames.append(fr)
                 hist = (hist + [x.readsample for x in self.field_log if x.valid])[-16:]
             self.stats['replay_s'] += time.perf_counter() - t0
+            if self.stats['batches'] % 32 == 0:
+                gc.collect(1)
             tf = time.perf_counter()
             self._flush(frames, W, H, sink)
             self.stats['flush_s'] = self.stats.get('flush_s', 0.0) + time.perf_counter() - tf

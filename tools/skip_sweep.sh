@@ -12,10 +12,12 @@ run() {
   [ $rc -eq 0 ] || { echo "rc $rc"; exit 1; }
 }
 run "demod only" LDG_STAGES=1
-run "all" LDG_STAGES=5
+run "demod+audio" LDG_STAGES=3
+run "demod+fields" LDG_STAGES=5
+run "all" LDG_STAGES=7
 i=0
 for k in sync_walk sync linelocs hsync_lines hsync_field philips burst_lines burst_field final_lines; do
-  run "skip $k" LDG_STAGES=5 LDG_SKIP=$((1 << i))
+  run "skip $k" LDG_STAGES=7 LDG_SKIP=$((1 << i))
   i=$((i+1))
 done
-run "skip all but sync_walk+sync" LDG_STAGES=5 LDG_SKIP=$((511 - 3))
+run "skip all but sync_walk+sync" LDG_STAGES=7 LDG_SKIP=$((511 - 3))
