@@ -185,7 +185,7 @@ class GPUDecoder:
         self.period, self.period_samples = P, D          # exact at 40 MSPS: 3 NTSC / 1 PAL frames
         self.field_nom = int(round(self.rf.freq_hz / self.sysp.fps / 2))
         self.trace = None          # diagnostics: planner steps (tools/miss_probe.py)
-        self.boot_wide = os.environ.get('LDG_BOOT_WIDE', '0') == '1'
+        self.boot_wide = os.environ.get('LDG_BOOT_WIDE', '1') == '1'   # +6.5% on the 60 s bench (tools/bootwide_ab.sh)
         self.comb, self.comb_sink = False, None
         self.comb3d = None                 # (core_ire, range_ire): the 3D comb (comb-ntsc -d 3 -F)
         self.pending = []                  # (keys, slots) of the outstanding decode launches, oldest first
