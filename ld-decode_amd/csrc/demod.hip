@@ -661,9 +661,14 @@ extern "C" __global__ __launch_bounds__(1024) void ldg_k_demod(
 // Audio phase 1 (lddecode_core.py:321-328): per overlap-save block, the two
 // carrier slices the demod filtered (aslice, 2 x 1024 bins) -> 1024-point IFFT
 // -> unwrap_hilbert at 2.5 MHz + the low carrier -> the block's kept audio
-// samples.  grid: n_reads * MAX_BLOCKS_PER_READ workgroups of 1024 threads
-// (threads [0,512) left, [512,1024) right).
-extern "C" __global__ __launch_bounds__(1024) void ldg_k_audio1(
+// samples.  grid: n_reads * MAX_BLOCKS_PER_READ workgroups of A1_T threads
+// (threads [0, A1_T/2) left, [A1_T/2, A1_T) right), 32 KiB of LDS: a 1024-point
+// radix-8 Stockham pass has 128 butterflies, so 128 threads per transform are
+// all busy and four workgroups share a CU.
+constexpr int A1_T = 256;
+constexpr int A1_H = A1_T / 2;
+constexpr int A1_P = 1024 / A1_H;      // points per thread
+extern "C" __global__ __launch_bounds__(A1_T) void ldg_k_audio1(
     const int32_t* __restrict__ smap, const ReadDesc* __restrict__ reads, const double2* __restrict__ tw, SysConst C,
     const double2* __restrict__ aslice, double* __restrict__ audio1, int64_t aread_stride, int64_t achan_stride,
     const int32_t* __restrict__ status) {
@@ -680,28 +685,28 @@ extern "C" __global__ __launch_bounds__(1024) void ldg_k_audio1(
   const double2* as = aslice + ((int64_t)slot * MAX_BLOCKS_PER_READ + b) * 2048;
   __shared__ double s_atan[65];
   if (tid < 65) s_atan[tid] = c_atan64[tid];   // ordered by the transform's first barrier
-  A_[tid] = as[tid];
-  A_[1024 + tid] = as[1024 + tid];
-  {
-    const int g = tid >> 9, lt = tid & 511;
-    const CBuf ga = A_ + (g ? 1024 : 0);
-    fft_lds<1024, 512, true>(ga, tw, lt);
-    double th[2];
 #pragma unroll
-    for (int e = 0; e < 2; e++) {
-      const double2 z = ga[lt + 512 * e];
+  for (int q = 0; q < 2048 / A1_T; q++) A_[tid + A1_T * q] = as[tid + A1_T * q];
+  {
+    const int g = tid / A1_H, lt = tid % A1_H;
+    const CBuf ga = A_ + (g ? 1024 : 0);
+    fft_lds<1024, A1_H, true>(ga, tw, lt);
+    double th[A1_P];
+#pragma unroll
+    for (int e = 0; e < A1_P; e++) {
+      const double2 z = ga[lt + A1_H * e];
       th[e] = kFastAtan2 ? fast_atan2(z.y, z.x, s_atan) : atan2(z.y, z.x);
     }
     __syncthreads();
     double* gth = reinterpret_cast<double*>(s_a) + (g ? 1024 : 0);     // plain (unswizzled) phase scratch
 #pragma unroll
-    for (int e = 0; e < 2; e++) gth[lt + 512 * e] = th[e];
+    for (int e = 0; e < A1_P; e++) gth[lt + A1_H * e] = th[e];
     __syncthreads();
     double* aout = audio1 + (int64_t)slot * aread_stride + (int64_t)g * achan_stride;
     const int kept = copylen / AUDIO_DIV1;
 #pragma unroll
-    for (int e = 0; e < 2; e++) {
-      const int p = lt + 512 * e;
+    for (int e = 0; e < A1_P; e++) {
+      const int p = lt + A1_H * e;
       const double prev = p ? gth[p - 1] : 0.0;
       const double d = p ? fold_tau(th[e] - prev) : 0.0;
       const double v = d * (C.freq_arf / TAU) + C.audio_lowfreq;
@@ -711,10 +716,9 @@ extern "C" __global__ __launch_bounds__(1024) void ldg_k_audio1(
     // zero the tail the reference leaves at 0 (np.zeros) after the last block
     if (b == rd.n_blocks - 1) {
       const int last = (off + copylen) / AUDIO_DIV1;
-      for (int j = last + lt; j < rd.n_audio; j += 512) aout[j] = 0.0;
+      for (int j = last + lt; j < rd.n_audio; j += A1_H) aout[j] = 0.0;
     }
   }
-
 }
 
 // ---------------------------------------------------------------------------
