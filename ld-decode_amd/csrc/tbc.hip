@@ -487,7 +487,11 @@ struct FinalLDS {
   double ra[FINAL_NT / 16], rb[FINAL_NT / 16];
   double m1, mn1;
 };
-extern "C" __global__ __launch_bounds__(FINAL_NT) void ldg_k_final_lines(
+#ifndef LDG_FINAL_WAVES
+#define LDG_FINAL_WAVES 6
+#endif
+// (6 waves per SIMD: 78 VGPRs, six line workgroups per CU, 138 KiB of LDS)
+extern "C" __global__ __launch_bounds__(FINAL_NT, LDG_FINAL_WAVES) void ldg_k_final_lines(
     const int32_t* __restrict__ smap, const double* __restrict__ video, int64_t vread_stride, int64_t vchan_stride,
     SysConst C, FieldRec* __restrict__ recs, const double* __restrict__ lines, const float* __restrict__ blevel,
     uint16_t* __restrict__ pic, int64_t pic_stride) {
@@ -537,7 +541,9 @@ extern "C" __global__ __launch_bounds__(FINAL_NT) void ldg_k_final_lines(
   const double M1 = S.m1, Mn1 = S.mn1;
   const double BL = M1, BR = Mn1;
   auto ct = [&](int t) { return t < 16 ? S.ct[t] : kCtInf; };
-  double rr[FINAL_CHMAX], cc[FINAL_CHMAX], dd[FINAL_CHMAX];
+  // (the Thomas coefficient c_t is re-read where used: it is constant past t = 16,
+  // and holding it per row would cost 22 VGPRs -- a wave per SIMD of occupancy)
+  double rr[FINAL_CHMAX], dd[FINAL_CHMAX];
 #pragma unroll
   for (int q = 0; q < FINAL_CHMAX; q++) {
     if (q < nq) {
@@ -546,15 +552,15 @@ extern "C" __global__ __launch_bounds__(FINAL_NT) void ldg_k_final_lines(
       if (t == 0) r -= BL;
       if (t == T - 1) r -= BR;
       rr[q] = r;
-      cc[q] = ct(t);
     }
   }
+  auto cc = [&](int q) { return ct(t0 + q); };
   // forward sweep: d -> -c d + c r
   double A = 1.0, B = 0.0;
 #pragma unroll
   for (int q = 0; q < FINAL_CHMAX; q++) {
     if (q < nq) {
-      const double c = cc[q];
+      const double c = cc(q);
       A = -c * A;
       B = (rr[q] - B) * c;
     }
@@ -563,7 +569,7 @@ extern "C" __global__ __launch_bounds__(FINAL_NT) void ldg_k_final_lines(
 #pragma unroll
   for (int q = 0; q < FINAL_CHMAX; q++) {
     if (q < nq) {
-      const double d = (rr[q] - dprev) * cc[q];
+      const double d = (rr[q] - dprev) * cc(q);
       dd[q] = d;
       dprev = d;
     }
@@ -573,7 +579,7 @@ extern "C" __global__ __launch_bounds__(FINAL_NT) void ldg_k_final_lines(
 #pragma unroll
   for (int q = FINAL_CHMAX - 1; q >= 0; q--) {
     if (q < nq) {
-      const double c = cc[q];
+      const double c = cc(q);
       A = -c * A;
       B = dd[q] - c * B;
     }
@@ -583,7 +589,7 @@ extern "C" __global__ __launch_bounds__(FINAL_NT) void ldg_k_final_lines(
 #pragma unroll
   for (int q = FINAL_CHMAX - 1; q >= 0; q--) {
     if (q < nq) {
-      const double M = dd[q] - cc[q] * Mnext;
+      const double M = dd[q] - cc(q) * Mnext;
       ms[lo + t0 + q] = M;
       Mnext = M;
     }
