@@ -32,6 +32,7 @@ NTSC_TBC_BYTES_PER_SAMPLE = 955500 / 1334667
 NTSC_PCM_BYTES_PER_SAMPLE = 0.0048
 NTSC_COMB_BYTES_PER_SAMPLE = (955500 + 2142720) / 1334667   # .tbc in + rgb48 out per frame
 BYTES_PER_SAMPLE = {0: 1.0, 1: 2.0, 2: 4 / 3, 3: 1.25}
+FMT_NAME = {0: 'u8', 1: 's16', 2: '10-bit .r30', 3: '10-bit .lds'}
 HBM_PEAK_GBS = 8000.0
 FP64_PEAK_TFLOPS = 78.6                           # MI355X FP64 vector (spec)
 READ_BLOCKS = 66                                  # overlap-save blocks per 1e6-sample field read
@@ -48,7 +49,9 @@ def parse():
     ap.add_argument('--warmup', type=int, default=1)
     ap.add_argument('--seconds', type=float, default=60.0)
     ap.add_argument('--batch', type=int, default=96)   # 80-96 measured ~5% over 64 (tools/batch_ab.sh)
-    ap.add_argument('--fmt', type=int, default=0)
+    ap.add_argument('--fmt', type=int, default=0, help='capture format: 0 u8, 1 s16, 2 .r30, 3 .lds (10-bit packed)')
+    ap.add_argument('--clv', action='store_true',
+                    help='CLV timecode instead of CAV picture numbers (captures past 79,999 frames, e.g. 1 h: config C5)')
     ap.add_argument('--cpu-seconds', type=float, default=1.0, help='oracle baseline sample (seconds of RF)')
     ap.add_argument('--no-cpu', action='store_true')
     ap.add_argument('--no-comb', action='store_true', help='stop at .tbc (skip the 2D comb stage)')
@@ -105,7 +108,7 @@ def main():
     nsamp = int(40e6 * args.seconds)
     t0 = time.perf_counter()
     # per-rank capture: its own CAV picture-number range and noise seed
-    dec.ctx.synth(nsamp, fmt=args.fmt, first_frame=1 + 2000 * (rank % 39), seed=20181015 + rank)
+    dec.ctx.synth(nsamp, fmt=args.fmt, first_frame=1 + 2000 * (rank % 39), clv=args.clv, seed=20181015 + rank)
     dec.use_resident_capture(args.fmt, nsamp)
     synth_s = time.perf_counter() - t0
     progress(rank, 'capture synthesised (%.1f s)' % synth_s)
@@ -160,6 +163,7 @@ def main():
             dist.destroy_process_group()
         return
 
+    disc = 'CLV' if args.clv else 'CAV'
     msps = consumed_all / dt_max / 1e6
     fields_s = 2 * frames_all / dt_max
     # roofline of the dominant kernel (HIP events around each launch, on the stream it runs on).
@@ -201,9 +205,10 @@ def main():
         'metric': 'RF Msamples/s (40 MSPS NTSC, full RF->.tbc decode)', 'value': round(msps, 3),
         'unit': 'RF Msamples/s', 'n_gpus': world, 'steps': args.steps, 'warmup': args.warmup,
         'ms_per_step': round(dt_max / args.steps * 1e3, 3), 'higher_is_better': True, 'scaling': 'weak',
-        'vs_baseline': None, 'dtype': 'f64', 'data': 'synthetic (GPU-synthesised NTSC CAV RF, u8)',
-        'config': {'workload': '%g s NTSC CAV, 40 MSPS 8-bit RF per GPU: RF->demod->TBC->.tbc+.pcm%s'
-                               % (args.seconds, '' if args.no_comb else '->2D comb rgb48'),
+        'vs_baseline': None, 'dtype': 'f64',
+        'data': 'synthetic (GPU-synthesised NTSC %s RF, %s)' % (disc, FMT_NAME[args.fmt]),
+        'config': {'workload': '%g s NTSC %s, 40 MSPS %s RF per GPU: RF->demod->TBC->.tbc+.pcm%s'
+                               % (args.seconds, disc, FMT_NAME[args.fmt], '' if args.no_comb else '->2D comb rgb48'),
                    'frames_per_step': frames // max(args.steps, 1), 'batch_reads': args.batch,
                    'parallelism': 'capture-sharded x%d' % world},
         'fields_per_s': round(fields_s, 1), 'realtime_x': round(msps / 40.0, 2),
@@ -216,7 +221,7 @@ def main():
                      'fp64': fp64},
         'kernels_ms': {k: round(v[1], 3) for k, v in sorted(stats.items(), key=lambda kv: -kv[1][1])},
         'cpu_baseline': cpu,
-        'checks': {'cav_framenr_consecutive': consecutive, 'synth_s': round(synth_s, 2),
+        'checks': {'framenr_consecutive': consecutive, 'synth_s': round(synth_s, 2),
                    'reads_decoded': dec.stats['reads'], 'reads_used': dec.stats['reads_used'],
                    'batches': dec.stats['batches'], 'misses': dec.stats.get('misses', 0),
                    'host_s': {k: round(dec.stats.get(k, 0.0), 4) for k in ('plan_s', 'gpu_s', 'replay_s', 'flush_s', 'wait_s')},

@@ -146,24 +146,28 @@ __device__ void chunk_freq(const SynthConst& S, const uint32_t* codes, int64_t n
 
 }  // namespace
 
+// Chunk index = blk0 + blockIdx.x: a launch's work-items stay below 2^32 (the
+// dispatch packet's grid size), so long captures (1 h = 35M chunks) take several launches.
 extern "C" __global__ __launch_bounds__(256) void ldg_k_synth_pass1(SynthConst S, const uint32_t* __restrict__ codes,
-                                                                    int64_t ncf, double* __restrict__ totals) {
+                                                                    int64_t ncf, double* __restrict__ totals, int64_t blk0) {
   __shared__ double x[SY_X], y[SY_N], carry[3 * SY_T];
-  const int64_t c0 = (int64_t)blockIdx.x * SY_CH;
+  const int64_t blk = blk0 + blockIdx.x;
+  const int64_t c0 = blk * SY_CH;
   chunk_freq(S, codes, ncf, c0, x, y, carry);
   // total phase advance over the chunk's SY_CH samples (fixed order, reused in pass 2)
   if (threadIdx.x == 0) {
     double tot = 0.0;
     for (int i = 0; i < SY_CH; i++) tot += (2 * 3.141592653589793 / SY_FS) * y[SY_WARM + i];
-    totals[blockIdx.x] = tot;
+    totals[blk] = tot;
   }
 }
 
 extern "C" __global__ __launch_bounds__(256) void ldg_k_synth_pass2(SynthConst S, const uint32_t* __restrict__ codes,
                                                                     int64_t ncf, const double* __restrict__ phase0,
-                                                                    int64_t nsamples, uint8_t* __restrict__ out) {
+                                                                    int64_t nsamples, uint8_t* __restrict__ out, int64_t blk0) {
   __shared__ double x[SY_X], y[SY_N], carry[3 * SY_T];
-  const int64_t c0 = (int64_t)blockIdx.x * SY_CH;
+  const int64_t blk = blk0 + blockIdx.x;
+  const int64_t c0 = blk * SY_CH;
   chunk_freq(S, codes, ncf, c0, x, y, carry);
   const int tid = threadIdx.x;
   // inclusive prefix of phase increments within the chunk (16 per thread + thread scan)
@@ -174,7 +178,7 @@ extern "C" __global__ __launch_bounds__(256) void ldg_k_synth_pass2(SynthConst S
   carry[tid] = s;
   __syncthreads();
   if (tid == 0) {
-    double acc = phase0[blockIdx.x];
+    double acc = phase0[blk];
     for (int t = 0; t < SY_T; t++) { const double v = carry[t]; carry[t] = acc; acc += v; }
   }
   __syncthreads();
@@ -212,8 +216,8 @@ extern "C" __global__ __launch_bounds__(256) void ldg_k_synth_pass2(SynthConst S
 
 // Pack staged 10-bit samples: fmt 2 = .r30 (3 per LE uint32), 3 = .lds (4 per 5 bytes).
 extern "C" __global__ void ldg_k_synth_pack10(const uint16_t* __restrict__ s, int64_t ngroups, int fmt,
-                                              uint8_t* __restrict__ out) {
-  const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+                                              uint8_t* __restrict__ out, int64_t g0) {
+  const int64_t g = g0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (g >= ngroups) return;
   if (fmt == 2) {
     const uint32_t w = (s[3 * g] & 0x3ffu) | ((uint32_t)(s[3 * g + 1] & 0x3ffu) << 10) |

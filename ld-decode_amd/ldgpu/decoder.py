@@ -364,7 +364,8 @@ class GPUDecoder:
 
     def _launch(self, keys, protect):
         """Decode `keys` now (launch and wait for everything outstanding)."""
-        self._launch_async(keys, protect)
+        while not self._launch_async(keys, protect):
+            self._launch_wait()
         while self.pending:
             self._launch_wait()
 
@@ -382,6 +383,8 @@ class GPUDecoder:
                 free.append(self.cache.pop(k)[0])      # oldest first (insertion / touch order)
             keys = keys[:len(free)]
         if not keys:
+            if self.pending:
+                return False                # every free slot is spoken for: wait for a launch first
             raise RuntimeError('read cache full (capacity %d)' % self.capacity)
         slots = free[:len(keys)]
         t0 = time.perf_counter()
@@ -391,6 +394,7 @@ class GPUDecoder:
         self.stats['reads'] += len(keys)
         self.pending.append((keys, slots))
         self.inflight.update(keys)
+        return True
 
     def _launch_wait(self):
         if not self.pending:
@@ -677,12 +681,12 @@ class GPUDecoder:
                 plan, chain = self._plan(nextsample, self.mtf_level, self.last_framenr, self.last_isclv, done == 0,
                                          want, hist, frames_left=num_frames - done + 2)
                 self.stats['plan_s'] = self.stats.get('plan_s', 0.0) + time.perf_counter() - tp
-                if not plan:
+                if not plan or not self._launch_async(plan, set(chain)):
                     break
-                self._launch_async(plan, set(chain))
                 launched += 1
             frames = []
             eof = False
+            missed = None
             t0 = time.perf_counter()
             self.requested = []
             while done + len(frames) < num_frames and self._tell() + bpf * 1.05 <= size and more(nextsample):
@@ -692,6 +696,7 @@ class GPUDecoder:
                 try:
                     fr = self.readframe(nextsample, firstframe and nframes_read == 0)
                 except Miss as m:
+                    missed = m.key
                     self._note_miss(m.key)
                     (nextsample, self.mtf_level, self.audio_offset, self.last_framenr, self.last_isclv,
                      self.last_read, nt, nframes_read) = cp
@@ -722,6 +727,11 @@ class GPUDecoder:
             if eof or (not frames and not launched and not self.pending):
                 break
             self._launch_wait()                 # the oldest launch: the replay continues into it
+            # the replay stopped at a read a newer launch holds: it cannot move before
+            # that launch lands, so wait for it rather than plan further ahead (each such
+            # plan pins another batch of cached reads; a long capture once filled the cache)
+            while missed is not None and missed in self.inflight and self.pending:
+                self._launch_wait()
         return done
 
     def _flush(self, frames, W, H, sink):
