@@ -141,6 +141,7 @@ def main():
     dt = time.perf_counter() - t0
     stats = dec.ctx.profile_stats()
     spans = dec.ctx.profile_spans()        # (launches, total ms) of the demod's execution spans
+    busy = dec.ctx.profile_spans_union()   # (launches, ms with at least one demod executing)
     dec.ctx.profile(False)
     reads_timed = dec.stats['reads'] - reads0
     # sanity on the full-size output: consecutive CAV picture numbers, all frames present
@@ -183,6 +184,11 @@ def main():
         bps += NTSC_COMB_BYTES_PER_SAMPLE
     units_per_launch = (consumed / max(args.steps, 1)) / max(dom_launches / max(args.steps, 1), 1)
     achieved = bps * units_per_launch / (avg_ms * 1e-3) / 1e9
+    # consecutive demod launches alternate between two streams and overlap: a launch's
+    # span includes time it shares with its neighbour.  The demod's own rate is the
+    # time with at least one launch executing, per launch (reported beside the contract figure)
+    busy_ms = busy[1] / busy[0] if (dom_name == 'demod' and busy[0]) else avg_ms
+    achieved_busy = bps * units_per_launch / (busy_ms * 1e-3) / 1e9
     traffic = None
     pmc = os.path.join(ROOT, 'profiles', 'pmc_traffic.json')
     if os.path.exists(pmc):
@@ -215,8 +221,12 @@ def main():
         'roofline': {'bound': 'hbm', 'kernel': dom_name, 'achieved': round(achieved, 4), 'peak': HBM_PEAK_GBS,
                      'unit': 'GB/s', 'frac': achieved / HBM_PEAK_GBS, 'traffic': traffic,
                      'avg_launch_ms': round(avg_ms, 4), 'launches': dom_launches,
-                     'timing': 'in-kernel execution span (device wall clock) per launch, HIP-event interval beside it',
+                     'timing': 'in-kernel execution span (device wall clock) per launch, HIP-event interval beside it; '
+                               'demod_busy_ms_per_launch: union of the spans (two demod streams overlap launches) / launches',
                      'hip_event_launch_ms': round(event_ms, 4), 'span_launches': spans[0],
+                     'demod_busy_ms_per_launch': round(busy_ms, 4), 'achieved_busy': round(achieved_busy, 4),
+                     'frac_busy': achieved_busy / HBM_PEAK_GBS,
+                     'demod_streams': int(os.environ.get('LDG_DEMOD_STREAMS', '2')),
                      'algorithmic_bytes_per_sample': round(bps, 4), 'traffic_unit': 'bytes per launch',
                      'fp64': fp64},
         'kernels_ms': {k: round(v[1], 3) for k, v in sorted(stats.items(), key=lambda kv: -kv[1][1])},

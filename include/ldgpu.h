@@ -253,6 +253,9 @@ int ldg_profile_read(ldg_ctx* ctx, ldg_kernel_stat* out, int max);
  * start to last workgroup end on the device's constant-rate clock, what a
  * kernel trace reports): count and summed milliseconds. */
 int ldg_profile_spans(ldg_ctx* ctx, double* total_ms, int64_t* count);
+/* The union of those spans (time with at least one demod launch executing; two
+ * demod streams overlap consecutive launches) and the launch count. */
+int ldg_profile_spans_union(ldg_ctx* ctx, double* union_ms, int64_t* count);
 
 /* ---- benchmark / test tooling (not a reference interface) ----------------------
  * Synthesise an NTSC LaserDisc RF capture directly into this context's HBM

@@ -22,7 +22,7 @@ EXPORTS = ['ldg_create', 'ldg_destroy', 'ldg_last_error', 'ldg_set_filters', 'ld
            'ldg_comb_ntsc', 'ldg_comb_reset', 'ldg_version', 'ldg_device_count', 'ldg_profile_enable',
            'ldg_profile_read', 'ldg_synth_capture', 'ldg_capture_download', 'ldg_comb_ntsc_async', 'ldg_sync',
            'ldg_archive_fields', 'ldg_archive_audio', 'ldg_decode_reads_async', 'ldg_decode_reads_wait',
-           'ldg_field_audio_async', 'ldg_field_audio_collect', 'ldg_comb_ntsc3d', 'ldg_cx_create', 'ldg_cx_destroy', 'ldg_cx_process', 'ldg_comb_pal', 'ldg_comb_set_state', 'ldg_profile_spans']
+           'ldg_field_audio_async', 'ldg_field_audio_collect', 'ldg_comb_ntsc3d', 'ldg_cx_create', 'ldg_cx_destroy', 'ldg_cx_process', 'ldg_comb_pal', 'ldg_comb_set_state', 'ldg_profile_spans', 'ldg_profile_spans_union']
 
 
 class FieldInfo(C.Structure):
@@ -109,6 +109,7 @@ def load(path=None):
     lib.ldg_profile_enable.argtypes = [vp, C.c_int]
     lib.ldg_profile_read.argtypes = [vp, C.POINTER(KernelStat), C.c_int]
     lib.ldg_profile_spans.argtypes = [vp, C.POINTER(C.c_double), C.POINTER(C.c_int64)]
+    lib.ldg_profile_spans_union.argtypes = [vp, C.POINTER(C.c_double), C.POINTER(C.c_int64)]
     lib.ldg_synth_capture.argtypes = [vp, C.POINTER(SynthParams), C.POINTER(C.c_double), C.POINTER(C.c_double),
                                       C.POINTER(C.c_uint32), C.c_int64]
     lib.ldg_capture_download.argtypes = [vp, vp, C.c_int64, C.c_int64]
@@ -354,6 +355,12 @@ class Context:
         """(count, total ms) of the demod launches' execution spans since profile(on)."""
         t, n = C.c_double(0), C.c_int64(0)
         self._check(self.lib.ldg_profile_spans(self.h, C.byref(t), C.byref(n)), 'ldg_profile_spans')
+        return int(n.value), float(t.value)
+
+    def profile_spans_union(self):
+        """(count, ms) of demod launches and the time at least one of them was executing."""
+        t, n = C.c_double(0), C.c_int64(0)
+        self._check(self.lib.ldg_profile_spans_union(self.h, C.byref(t), C.byref(n)), 'ldg_profile_spans_union')
         return int(n.value), float(t.value)
 
     def profile_stats(self):
