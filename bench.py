@@ -203,7 +203,9 @@ def main():
         blocks = reads_timed * READ_BLOCKS
         flops = blocks * DEMOD_FLOPS_PER_BLOCK
         tf = flops / (stats['demod'][1] * 1e-3) / 1e12
+        tf_busy = flops / (busy[1] * 1e-3) / 1e12 if busy[1] else tf
         fp64 = {'kernel': 'demod', 'achieved_tflops': round(tf, 3), 'peak_tflops': FP64_PEAK_TFLOPS,
+                'achieved_tflops_busy': round(tf_busy, 3), 'frac_busy': tf_busy / FP64_PEAK_TFLOPS,
                 'frac': tf / FP64_PEAK_TFLOPS, 'flops_per_block': DEMOD_FLOPS_PER_BLOCK,
                 'blocks_per_launch': blocks / stats['demod'][0]}
     cpu = None if args.no_cpu else cpu_baseline(args.cpu_seconds)
