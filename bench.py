@@ -140,6 +140,11 @@ def main():
     barrier()
     dt = time.perf_counter() - t0
     stats = dec.ctx.profile_stats()
+    if dec.htrace is not None:                 # LDG_HOSTTRACE=<file>: the host timeline of the timed steps
+        with open(os.environ['LDG_HOSTTRACE'], 'w') as f:
+            for t, ev, n in dec.htrace:
+                if t >= t0:
+                    f.write('%.4f %s %d\n' % ((t - t0) * 1e3, ev, n))
     spans = dec.ctx.profile_spans()        # (launches, total ms) of the demod's execution spans
     busy = dec.ctx.profile_spans_union()   # (launches, ms with at least one demod executing)
     dec.ctx.profile(False)
@@ -236,6 +241,7 @@ def main():
         'checks': {'framenr_consecutive': consecutive, 'synth_s': round(synth_s, 2),
                    'reads_decoded': dec.stats['reads'], 'reads_used': dec.stats['reads_used'],
                    'batches': dec.stats['batches'], 'misses': dec.stats.get('misses', 0),
+                   'drain_waits': dec.stats.get('drain_waits', 0),
                    'host_s': {k: round(dec.stats.get(k, 0.0), 4) for k in ('plan_s', 'gpu_s', 'replay_s', 'flush_s', 'wait_s')},
                    'miss_sample': dec.stats.get('miss_log', [])[:12],
                    'inflight_at_wait': dec.stats.get('inflight_at_wait')},

@@ -186,6 +186,8 @@ class GPUDecoder:
         self.field_nom = int(round(self.rf.freq_hz / self.sysp.fps / 2))
         self.trace = None          # diagnostics: planner steps (tools/miss_probe.py)
         self.boot_wide = os.environ.get('LDG_BOOT_WIDE', '1') == '1'   # +6.5% on the 60 s bench (tools/bootwide_ab.sh)
+        self.miss_drain = os.environ.get('LDG_MISS_DRAIN', '1') == '1'
+        self.htrace = [] if os.environ.get('LDG_HOSTTRACE') else None   # (perf_counter, event, n): host timeline
         self.comb, self.comb_sink = False, None
         self.comb3d = None                 # (core_ire, range_ire): the 3D comb (comb-ntsc -d 3 -F)
         self.pending = []                  # (keys, slots) of the outstanding decode launches, oldest first
@@ -390,6 +392,8 @@ class GPUDecoder:
         t0 = time.perf_counter()
         self.ctx.decode_reads_async([k[0] for k in keys], [k[1] for k in keys], slots)
         self.stats['gpu_s'] += time.perf_counter() - t0
+        if self.htrace is not None:
+            self.htrace.append((t0, 'launch', len(keys)))
         self.stats['batches'] += 1
         self.stats['reads'] += len(keys)
         self.pending.append((keys, slots))
@@ -405,6 +409,9 @@ class GPUDecoder:
         t0 = time.perf_counter()
         infos = self.ctx.decode_reads_wait()
         self.stats['wait_s'] = self.stats.get('wait_s', 0.0) + time.perf_counter() - t0
+        if self.htrace is not None:
+            self.htrace.append((t0, 'wait', len(keys)))
+            self.htrace.append((time.perf_counter(), 'waited', len(keys)))
         self.inflight.difference_update(keys)
         import bisect
         for k, sl, inf in zip(keys, slots, infos):
@@ -720,8 +727,13 @@ class GPUDecoder:
             if self.stats['batches'] % 32 == 0:
                 gc.collect(1)
             tf = time.perf_counter()
+            if self.htrace is not None:
+                self.htrace.append((t0, 'replay', len(frames)))
+                self.htrace.append((tf, 'flush', len(frames)))
             self._flush(frames, W, H, sink)
             self.stats['flush_s'] = self.stats.get('flush_s', 0.0) + time.perf_counter() - tf
+            if self.htrace is not None:
+                self.htrace.append((time.perf_counter(), 'flushed', len(frames)))
             done += len(frames)
             self.stats['reads_used'] += sum(len(f.fields) for f in frames)
             if eof or (not frames and not launched and not self.pending):
@@ -730,7 +742,8 @@ class GPUDecoder:
             # the replay stopped at a read a newer launch holds: it cannot move before
             # that launch lands, so wait for it rather than plan further ahead (each such
             # plan pins another batch of cached reads; a long capture once filled the cache)
-            while missed is not None and missed in self.inflight and self.pending:
+            while self.miss_drain and missed is not None and missed in self.inflight and self.pending:
+                self.stats['drain_waits'] = self.stats.get('drain_waits', 0) + 1
                 self._launch_wait()
         return done
 
