@@ -187,6 +187,7 @@ class GPUDecoder:
         self.trace = None          # diagnostics: planner steps (tools/miss_probe.py)
         self.boot_wide = os.environ.get('LDG_BOOT_WIDE', '1') == '1'   # +6.5% on the 60 s bench (tools/bootwide_ab.sh)
         self.miss_drain = os.environ.get('LDG_MISS_DRAIN', '1') == '1'
+        self.plan_located = 0              # leading fields the last plan walked on decoded reads
         self.htrace = [] if os.environ.get('LDG_HOSTTRACE') else None   # (perf_counter, event, n): host timeline
         self.comb, self.comb_sink = False, None
         self.comb3d = None                 # (core_ire, range_ire): the 3D comb (comb-ntsc -d 3 -F)
@@ -231,6 +232,7 @@ class GPUDecoder:
 
     def _reset_cache(self):
         self.cache, self.hints, self._hint_keys = {}, {}, []
+        self.plan_located = 0
 
     # ---- forward simulator (plans the next GPU launch) ---------------------------
     def _next_known(self, start, info):
@@ -277,6 +279,7 @@ class GPUDecoder:
         frames_left: the decode stops after this many more frames (lddecode.py:49,88 num_frames),
         so reads past that frame are never needed."""
         new, seen, chain = [], set(), []
+        located, guessing = 0, False   # leading steps resolved by a decoded read (hit or hint)
         starts = list(hist)
         # the replay stops once the last read's fd.tell() + 1.05 frames passes the
         # file size (lddecode.py:89): plan at most the rest of that frame beyond it
@@ -298,17 +301,23 @@ class GPUDecoder:
                     seen.add(key)
                     new.append(key)
                     if len(new) >= want:
+                        self.plan_located = located
                         return new, chain
                     if self.cap_nsamples is not None and read_geometry(key[0])[2] + BLOCKLEN > self.cap_nsamples:
+                        self.plan_located = located
                         return new, chain     # this read's last block passes the capture end (EOF)
                     if limit is not None and loader_tell(self.fmt, read_geometry(key[0])[2], self.cap_bytes) > limit:
                         past_limit += 1
                         if past_limit > 3:
+                            self.plan_located = located
                             return new, chain
                 if hit is not None:
                     chain.append(key)
+                    if not guessing:
+                        located += 1
                     info = hit[1]
                     if info.status == native.FS_EOF or info.status == native.FS_CRASH:
+                        self.plan_located = located
                         return new, chain
                     nxt = self._next_known(key[0], info)
                     valid = info.status == native.FS_VALID
@@ -319,12 +328,15 @@ class GPUDecoder:
                     h = self._hint(key[0])
                     if h is not None and h[1].status == native.FS_VALID:
                         # a decoded read of the same field: its next start, parity and VBI
+                        if not guessing:
+                            located += 1
                         nxt, hinfo = h
                         valid = True
                         istop = bool(hinfo.istop)
                         fnr = hinfo.vbi_framenr if hinfo.vbi_framenr != native.VBI_NONE else None
                         clv = bool(hinfo.vbi_isclv)
                     else:
+                        guessing = True
                         if h is not None:
                             nxt = h[0]
                         elif len(starts) >= self.period - 1:
@@ -362,6 +374,7 @@ class GPUDecoder:
                         newmtf = 0
                     cur_mtf = newmtf
             firstframe = False
+        self.plan_located = located
         return new, chain
 
     def _launch(self, keys, protect):
@@ -677,9 +690,12 @@ class GPUDecoder:
             # while the older one's field kernels finish and the host replays.
             steady = len(hist) >= self.period + 2
             if self.boot_wide and not steady:
-                # P + 2 decoded reads (hints) already locate the next fields exactly and
-                # seed the period extrapolation: go wide before the replay catches up
-                steady = len(self._hint_keys) >= self.period + 2
+                # once the last plan walked P + 2 fields on decoded reads (cache hits or
+                # hints within 4096 samples), the next fields are located exactly and the
+                # period extrapolation is seeded: go wide before the replay catches up.
+                # (Counting hints alone went wide on the boot launch's nominal-spacing
+                # guesses for PAL, P + 2 = 4, and wasted two whole batches.)
+                steady = self.plan_located >= self.period + 2
             depth = self.depth if steady else 1
             launched = 0
             while len(self.pending) < depth:
