@@ -90,7 +90,7 @@ class GPUField:
     The VBI / line-code dicts are built on first use."""
 
     __slots__ = ('info', 'slot', 'readsample', 'mtf_level', 'audio_offset', 'valid', 'istop', 'linecount',
-                 'nextfieldoffset', 'npeaks', 'nvsync', '_vbi', '_linecode', 'tbcstart', 'status',
+                 'nextfieldoffset', 'npeaks', 'nvsync', 'vbi', '_linecode', 'tbcstart', 'status',
                  'audio_next_offset', 'nextsample', 'dsaudio_used', 'tidx', 'sysp')
 
     def __init__(self, info, slot, readsample, mtf, audio_offset, sysp, frametime_lines):
@@ -105,26 +105,21 @@ class GPUField:
         self.tbcstart = info.tbcstart
         self.dsaudio_used = False
         self.sysp = sysp
-        self._vbi = self._linecode = None
+        self._linecode = None
+        self.vbi = None
         if self.valid:
+            # the VBI dict (a plain attribute: the replay reads it ~18 times per frame)
+            def v(x):
+                return None if x == native.VBI_NONE else int(x)
+            self.vbi = {'minutes': v(info.vbi_minutes), 'seconds': v(info.vbi_seconds),
+                        'clvframe': v(info.vbi_clvframe), 'framenr': v(info.vbi_framenr),
+                        'statuscode': None, 'status': v(info.vbi_status), 'isclv': bool(info.vbi_isclv)}
             # downscale_audio's returned next offset (lddecode_core.py:432-437,484)
             frametime = (sysp.line_period * self.linecount) / 1000000
             gap = 1 / 48000.0
             self.audio_next_offset = arange_last(audio_offset, frametime + gap, gap) - frametime
         else:
             self.audio_next_offset = audio_offset
-
-    @property
-    def vbi(self):
-        if self._vbi is None and self.valid:
-            info = self.info
-
-            def v(x):
-                return None if x == native.VBI_NONE else int(x)
-            self._vbi = {'minutes': v(info.vbi_minutes), 'seconds': v(info.vbi_seconds),
-                         'clvframe': v(info.vbi_clvframe), 'framenr': v(info.vbi_framenr),
-                         'statuscode': None, 'status': v(info.vbi_status), 'isclv': bool(info.vbi_isclv)}
-        return self._vbi
 
     @property
     def linecode(self):
@@ -530,16 +525,18 @@ class GPUDecoder:
             self.transitions.append(int(f.linecount))   # offset -> next(offset, linecount)
         vbi = self.mergevbi(fields)
         self.vbi = vbi
-        self.last_isclv = bool(f.vbi['isclv'])
-        if f.vbi['framenr'] is not None:
-            self.last_framenr = f.vbi['framenr']
-        if not f.vbi['isclv'] and f.vbi['framenr'] is not None:
-            newmtf = 1 - (f.vbi['framenr'] / 10000)
+        fv = f.vbi
+        self.last_isclv = bool(fv['isclv'])
+        fnr = fv['framenr']
+        if fnr is not None:
+            self.last_framenr = fnr
+        if not fv['isclv'] and fnr is not None:
+            newmtf = 1 - (fnr / 10000)
             if newmtf < 0:
                 newmtf = 0
             oldmtf = self.mtf_level
             self.mtf_level = newmtf
-            if np.abs(newmtf - oldmtf) > .1:
+            if abs(newmtf - oldmtf) > .1:
                 return self.readframe(sample, firstframe, cav)
         return FrameOut(top=fields[0], bottom=fields[1], audio_fields=audio, vbi=vbi, nextsample=sample)
 

@@ -23,7 +23,8 @@ def main():
     t0 = time.perf_counter()
     data = make_capture(int(40e6 * secs), 'u8', system='PAL', clv=True, first_frame=3000, seed=20181018)
     synth_s = time.perf_counter() - t0
-    dec = GPUDecoder(system='PAL', batch=96)
+    batch = int(sys.argv[sys.argv.index('--batch') + 1]) if '--batch' in sys.argv else 96
+    dec = GPUDecoder(system='PAL', batch=batch)
     dec.set_capture(data, 0)
     dec._reset_cache()
     dec.decode(sink=None)                              # warm-up

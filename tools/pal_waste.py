@@ -37,6 +37,12 @@ def main():
     us = set(used)
     print('frames %d, launches %d, reads %d, used %d, unused %d' % (n, len(launched), len(allk), len(us), len([k for k in allk if k not in us])))
     last_used = max(k[0] for k in us)
+    seq = sorted(k[0] for k in us)
+    import collections
+    for P in (2, 4, 8):
+        d = collections.Counter(seq[i + P] - seq[i] for i in range(len(seq) - P))
+        print('r[k+%d] - r[k]: %s' % (P, d.most_common(6)))
+    print('first diffs', [seq[i + 1] - seq[i] for i in range(min(30, len(seq) - 1))])
     for i, b in enumerate(launched):
         un = [k for k in b if k not in us]
         past = sum(1 for k in un if k[0] > last_used)
