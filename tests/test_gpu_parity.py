@@ -183,3 +183,21 @@ def test_gpu_synth_10bit_formats(fmt):
     dec.decode(sink=lambda fr, au, m: got.append(m))
     assert len(got) >= 2
     assert [m['vbi']['framenr'] for m in got] == list(range(8, 8 + len(got)))
+
+
+@pytest.mark.parametrize('clv', [False, True])
+def test_gpu_long_capture_decodes_every_frame(clv):
+    """A 5-minute capture (12 GB u8, past the ~3000-frame point where the planner once
+    pinned the whole read cache) decodes every frame the reference's EOF guard allows,
+    with consecutive picture numbers / CLV timecodes, in benchmark mode (frames in HBM)."""
+    from ldgpu.decoder import GPUDecoder
+    n = int(40e6 * 300)
+    dec = GPUDecoder(system='NTSC', batch=128)
+    dec.ctx.synth(n, fmt=0, first_frame=1, clv=clv, seed=21)
+    dec.use_resident_capture(0, n)
+    nfr = dec.decode(sink=None)
+    bpf = dec.rf.samples_per_frame * 5 // 4            # lddecode.py:42 (10-bit packing assumed)
+    assert nfr == n // bpf - 1 or nfr == n // bpf, (nfr, n // bpf)
+    nrs = dec.frame_numbers
+    assert len(nrs) == nfr and all(b == a + 1 for a, b in zip(nrs, nrs[1:]))
+    assert dec.stats['reads'] < 1.02 * dec.stats['reads_used']
