@@ -127,6 +127,10 @@ __device__ __forceinline__ Slot slot_of(int tid, int c) {
 // This workgroup's physical CU: (XCC, SE, SH, CU) from HW_REG_XCC_ID / HW_REG_HW_ID
 // (gfx9 HW_ID: CU_ID [11:8], SH_ID [12], SE_ID [15:13]), < PARK_SLOTS.
 constexpr int PARK_SLOTS = 2048;
+// One park per CU is private only while two demod workgroups can never share a CU
+// (also across the two demod streams' concurrent launches): the transform buffer
+// alone is more than half of the CU's 160 KiB of LDS.
+static_assert(sizeof(double2) * HALF > 160 * 1024 / 2, "demod workgroups must not share a CU");
 __device__ __forceinline__ int cu_slot() {
   const unsigned hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);
   const unsigned xcc = __builtin_amdgcn_s_getreg((31 << 11) | 20);
