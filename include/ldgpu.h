@@ -194,7 +194,9 @@ int ldg_assemble_frames(ldg_ctx* ctx, int n, const int32_t* top_slots, const int
  * what: 0..4 demod channels (demod, demod_05, demod_sync, demod_burst, demod_pilot)
  *       [float64, n_out]; 10,11: audio_left/right after phase 2 [float64];
  *       20..24: linelocs1, linelocs2, linelocs3, linelocs4, final linelocs [float64];
- *       30: burstlevel [float32]; 31: linebad [int8]; 40: dspicture [uint16]; 41: peaklist [int32].
+ *       30: burstlevel [float32]; 31: linebad [int8]; 40: dspicture [uint16]; 41: peaklist [int32];
+ *       50: the last ldg_comb_ntsc[3d] call's burst-level EMA per line (lines 38..524 of each
+ *       frame) [float64]; 51: the comb's carried EMA state [float64] (50 and 51 ignore `slot`).
  * Copies up to `cap` bytes to host `dst`; returns bytes copied (>= 0) or an error. */
 int64_t ldg_debug_read(ldg_ctx* ctx, int slot, int what, void* dst, int64_t cap);
 

@@ -135,70 +135,87 @@ using namespace ldg::comb;
 // aburstlev chain (ToRGB :560-566) over lines 38..524 of n frames in order.
 // state[0]: aburstlev carried across calls (-1 = not initialised).
 // abl[f * CHAIN_LINES + (l - 38)]: the value ToRGB uses for line l of frame f.
-// The recurrence is exact and sequential: 256 threads stage the burst levels
-// of a chunk in LDS, thread 0 runs the chain over them (the loads are off the
-// dependency path, so it runs at the FP64 mul+add latency), all threads write
-// the results back.  grid: 1 workgroup of 256 threads.
-constexpr int BURST_CHUNK = 4096;
+//
+// The recurrence is sequential in the reference and must stay bit-exact, but it
+// forgets: two runs of it over the same levels from different states differ by
+// 0.99^k after k qualifying lines, and once their difference is below an ulp
+// they round to the same double and stay identical from then on.  So the lines
+// of a piece are split into 256 chunks, one per thread; thread j starts `warm`
+// lines before its chunk (from the piece's true state when that reaches back to
+// the piece start, else from "not initialised") and runs the chain through its
+// chunk.  Its state entering the chunk equals the state thread j-1 ends with iff
+// the two runs have met, and then thread j's chunk is exactly the sequential
+// chain's (by induction from chunk 0, which starts from the true state).  A chunk
+// whose check fails is recomputed, with everything after it, sequentially by
+// thread 0 from the verified state before it (the round-1 kernel's path).  With
+// warm = 5120 a run from a guess within a few IRE meets the true one after
+// ~3500 qualifying lines, so the serial path is a fallback; LDG_COMB_WARM small
+// forces it (tests).  About warm + total/256 steps per thread instead of total
+// steps on one lane: ~6k instead of ~30k for a 60-frame call.
+// grid: 1 workgroup of 256 threads.
+constexpr int BURST_PIECE = 40960;   // lines staged per pass (80 KiB of uint16 levels in LDS)
+__device__ __forceinline__ double burst_step(double a, uint16_t raw) {
+  const double bk = raw / IRESCALE;                    // comb-ntsc.cxx:560
+  const double base = (a < 0) ? bk : a;                // :563 (first qualifying line)
+  const double e = (base * .99) + (bk * .01);          // :564
+  return (bk > 3) ? e : a;
+}
 extern "C" __global__ __launch_bounds__(256) void ldg_k_comb_burst(const uint16_t* __restrict__ frames, int n,
                                                                    double* __restrict__ state,
-                                                                   double* __restrict__ abl) {
+                                                                   double* __restrict__ abl, int warm) {
   prio_latency();
 
-  __shared__ __align__(16) double s_b[BURST_CHUNK];
-  __shared__ __align__(16) double s_a[BURST_CHUNK];
+  __shared__ uint16_t s_u[BURST_PIECE];
+  __shared__ double s_in[256], s_out[256];
+  __shared__ int s_bad;
   const int tid = threadIdx.x;
-  double a = state[0];
+  double a_in = state[0];
   const int total = n * CHAIN_LINES;
-  for (int c0 = 0; c0 < total; c0 += BURST_CHUNK) {
-    const int cnt = (total - c0) < BURST_CHUNK ? (total - c0) : BURST_CHUNK;
+  for (int p0 = 0; p0 < total; p0 += BURST_PIECE) {
+    const int cnt = (total - p0) < BURST_PIECE ? (total - p0) : BURST_PIECE;
     for (int k = tid; k < cnt; k += 256) {
-      const int j = c0 + k;
+      const int j = p0 + k;
       const int f = j / CHAIN_LINES, l = FIRST_LINE + j % CHAIN_LINES;
-      s_b[k] = frames[(size_t)f * IN_X * IN_Y + (size_t)l * IN_X + 1] / IRESCALE;
+      s_u[k] = frames[(size_t)f * IN_X * IN_Y + (size_t)l * IN_X + 1];
+    }
+    if (tid == 0) s_bad = cnt;
+    __syncthreads();
+    const int L = (cnt + 255) / 256;
+    const int c0 = tid * L, c1 = (c0 + L) < cnt ? c0 + L : cnt;
+    if (c0 < cnt) {
+      const int w = (c0 - warm) > 0 ? c0 - warm : 0;
+      double a = (w == 0) ? a_in : -1.0;
+#pragma unroll 8
+      for (int k = w; k < c0; k++) a = burst_step(a, s_u[k]);
+      s_in[tid] = a;
+#pragma unroll 8
+      for (int k = c0; k < c1; k++) {
+        a = burst_step(a, s_u[k]);
+        abl[p0 + k] = a;
+      }
+      s_out[tid] = a;
     }
     __syncthreads();
-    if (tid == 0) {
-      int k = 0;
-      for (; k < cnt && a < 0; k++) {       // until the first qualifying line sets it
-        const double bk = s_b[k];
-        if (bk > 3) {
-          a = bk;
-          a = (a * .99) + (bk * .01);
-        }
-        s_a[k] = a;
-      }
-      // a > 0 from here on (burst levels > 3): only the EMA is on the serial path;
-      // levels are read and results written 16 at a time (16-byte LDS accesses)
-      auto step = [&](double bk) {
-        const double e = (a * .99) + (bk * .01);
-        a = (bk > 3) ? e : a;
-        return a;
-      };
-      if (k < cnt && (k & 1)) { s_a[k] = step(s_b[k]); k++; }
-#pragma unroll 1
-      for (; k + 16 <= cnt; k += 16) {
-        double bs[16];
-#pragma unroll
-        for (int j = 0; j < 16; j += 2) {
-          const double2 v = *reinterpret_cast<const double2*>(s_b + k + j);
-          bs[j] = v.x;
-          bs[j + 1] = v.y;
-        }
-#pragma unroll
-        for (int j = 0; j < 16; j += 2) {
-          const double a0 = step(bs[j]);
-          const double a1 = step(bs[j + 1]);
-          *reinterpret_cast<double2*>(s_a + k + j) = make_double2(a0, a1);
-        }
-      }
-      for (; k < cnt; k++) s_a[k] = step(s_b[k]);
-    }
+    if (tid > 0 && c0 < cnt && __double_as_longlong(s_in[tid]) != __double_as_longlong(s_out[tid - 1]))
+      atomicMin(&s_bad, c0);
     __syncthreads();
-    for (int k = tid; k < cnt; k += 256) abl[c0 + k] = s_a[k];
+    const int bad = s_bad;
+    const int last = (cnt - 1) / L;                     // the thread holding the piece's last line
+    if (bad < cnt) {
+      if (tid == 0) {
+        double a = s_out[bad / L - 1];
+        for (int k = bad; k < cnt; k++) {
+          a = burst_step(a, s_u[k]);
+          abl[p0 + k] = a;
+        }
+        s_out[last] = a;
+      }
+      __syncthreads();
+    }
+    a_in = s_out[last];
     __syncthreads();
   }
-  if (tid == 0) state[0] = a;
+  if (tid == 0 && total > 0) state[0] = a_in;
 }
 
 // ---- ldg_k_comb_split: SplitIQ's signed chroma of one row.

@@ -265,3 +265,59 @@ def test_gpu_comb_set_state_continues_the_chain(gpu_ctx_ntsc):
     part = ctx.comb_ntsc(fr[2:])
     assert np.array_equal(full[2:], part)
     ctx.comb_reset()
+
+
+# ---- the burst-level EMA chain (ldg_k_comb_burst: speculative chunks + exact check) ----
+
+def _burst_frames(n, seed):
+    """n frames whose line burst levels (px 1) are random: 15-30 IRE, with ~20% of lines
+    at or below the 3 IRE qualification (the EMA holds there) and the first 700 lines of
+    the sequence unqualified (the chain starts uninitialised)."""
+    rng = np.random.default_rng(seed)
+    fr = np.repeat(frame_solid(50.0, 800, -400)[None], n, axis=0)
+    lv = rng.uniform(15.0, 30.0, (n, 525))
+    lv[rng.random((n, 525)) < 0.2] = rng.uniform(0.0, 3.0)
+    lv.reshape(-1)[:700] = 1.0
+    fr[:, :, 1] = (lv * IRESCALE).astype(np.uint16)
+    return fr
+
+
+def _chain_values(a, frames):
+    """The reference's EMA (comb-ntsc.cxx:560-566) over lines 38..524, value per line."""
+    out = []
+    for b in (frames[:, 38:525, 1].astype(np.float64) / IRESCALE).reshape(-1).tolist():
+        if b > 3:
+            if a < 0:
+                a = b
+            a = (a * .99) + (b * .01)
+        out.append(a)
+    return np.array(out), a
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('warm', [None, 16])
+def test_gpu_comb_burst_chain_bit_exact(warm, monkeypatch):
+    """The parallel EMA kernel equals the sequential chain bit for bit: over a call of 100
+    frames (two LDS pieces, 48,700 lines), after a short call that initialised the state,
+    with the default run-in (the speculative chunks meet the true chain) and with
+    LDG_COMB_WARM=16 (almost every chunk fails its check: the serial fix-up path)."""
+    from ldgpu import native
+    from ldgpu.rfparams import RFTables
+    if warm is not None:
+        monkeypatch.setenv('LDG_COMB_WARM', str(warm))
+    rf = RFTables('NTSC')
+    ctx = native.Context('NTSC', 0, max_reads=4, max_frames=100)
+    ctx.set_filters(rf.params(), rf.tables)
+    fr = _burst_frames(103, seed=31 if warm is None else 32)
+    ctx.comb_reset()
+    ref, a = _chain_values(-1.0, fr[:3])
+    ctx.comb_ntsc(fr[:3])
+    got = ctx.debug(0, 50, np.float64, 3 * 487)
+    assert np.array_equal(got.view(np.int64), ref.view(np.int64))
+    ref, a = _chain_values(a, fr[3:])
+    ctx.comb_ntsc(fr[3:])
+    got = ctx.debug(0, 50, np.float64, 100 * 487)
+    st = ctx.debug(0, 51, np.float64, 1)
+    assert got.size == ref.size
+    assert np.array_equal(got.view(np.int64), ref.view(np.int64)), np.flatnonzero(got != ref)[:10]
+    assert st[0] == a
