@@ -696,10 +696,22 @@ class GPUDecoder:
             depth = self.depth if steady else 1
             launched = 0
             while len(self.pending) < depth:
-                want = self.batch if steady else min(self.batch, 8 if self._hint_keys else 4)
+                # boot: the first launch holds P + 2 reads (the first read and P + 1 guesses at the
+                # nominal field spacing, whose decoded records locate the next fields exactly when
+                # the capture starts near a field start); later boot plans are walked wide and
+                # launched wide when this very walk located P + 2 fields on decoded reads, else
+                # cut to the narrow size (a walk's first keys do not depend on how far it goes)
+                narrow = min(self.batch, 8 if self._hint_keys else self.period + 2)
+                probe_wide = not steady and self.boot_wide and bool(self._hint_keys)
+                want = self.batch if (steady or probe_wide) else narrow
                 tp = time.perf_counter()
                 plan, chain = self._plan(nextsample, self.mtf_level, self.last_framenr, self.last_isclv, done == 0,
                                          want, hist, frames_left=num_frames - done + 2)
+                if probe_wide:
+                    if self.plan_located >= self.period + 2:
+                        steady, depth = True, self.depth
+                    else:
+                        plan = plan[:narrow]
                 self.stats['plan_s'] = self.stats.get('plan_s', 0.0) + time.perf_counter() - tp
                 if not plan or not self._launch_async(plan, set(chain)):
                     break
