@@ -33,6 +33,11 @@ CASES = {
     'ntsc_cav_lds_0p15s': dict(seconds=0.15, fmt='lds', system='NTSC', kw={'seed': 8}),
     'pal_clv_u8_0p2s': dict(seconds=0.2, fmt='u8', system='PAL',
                             kw={'clv': True, 'first_frame': 3000, 'seed': 5}),
+    # the s16 loader (lddutils.py:131-147)
+    'ntsc_cav_s16_0p15s': dict(seconds=0.15, fmt='s16', system='NTSC', kw={'seed': 9}),
+    # a capture that starts 300,000 samples into a field (the first read's short
+    # nextfieldoffset, demod's start-1024 quirk at the file start, lddecode_core.py:378-380)
+    'ntsc_cav_u8_mid_0p2s': dict(seconds=0.2, fmt='u8', system='NTSC', kw={'seed': 10}, skip=300000),
 }
 
 
@@ -42,7 +47,12 @@ def sha(b):
 
 def build_capture(case):
     c = CASES[case]
-    return make_capture(int(40e6 * c['seconds']), c['fmt'], system=c['system'], **c['kw'])
+    skip = c.get('skip', 0)
+    data = make_capture(int(40e6 * c['seconds']) + skip, c['fmt'], system=c['system'], **c['kw'])
+    if skip:
+        assert c['fmt'] in ('u8', 's16')
+        data = data[skip * (2 if c['fmt'] == 's16' else 1):]
+    return data
 
 
 def make(case):

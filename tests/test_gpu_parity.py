@@ -101,7 +101,8 @@ def test_tbc_lines_and_audio(decoded):
 
 
 @pytest.mark.parametrize('case', ['ntsc_cav_u8_0p2s', 'ntsc_clv_u8_0p2s', 'ntsc_cav_r30_0p15s',
-                                  'ntsc_cav_lds_0p15s', 'pal_clv_u8_0p2s'])
+                                  'ntsc_cav_lds_0p15s', 'pal_clv_u8_0p2s', 'ntsc_cav_s16_0p15s',
+                                  'ntsc_cav_u8_mid_0p2s'])
 @pytest.mark.parametrize("batch", [3, 16])
 def test_end_to_end_vs_golden(case, batch):
     """Full decode (speculative batches) vs the oracle's committed golden output."""
@@ -148,6 +149,32 @@ def test_end_to_end_pixels_vs_oracle(cav_capture):
         assert np.abs(au.astype(np.int64) - a.astype(np.int64)).max() <= 1
         assert m == om
     print('bit-exact frames: %d/%d' % (exact, len(frames)))
+
+
+@pytest.mark.parametrize('case', ['ntsc_cav_s16_0p15s', 'ntsc_cav_u8_mid_0p2s'])
+def test_edge_captures_pixels_vs_oracle(case):
+    """The s16 loader and a capture starting mid-field (first read's short next-field
+    offset, demod's start-1024 quirk at the file start): pixels within +-1 LSB, audio
+    within +-1 and metadata exact against a fresh oracle decode."""
+    import sys
+    sys.path.insert(0, os.path.join(HERE, 'golden'))
+    import make_golden
+    from ldgpu.decoder import GPUDecoder
+    from ldgpu.formats import NAME_TO_FMT
+    from oracle.capture import FMT_BY_EXT
+    from oracle.framer import decode_capture
+    c = make_golden.CASES[case]
+    data = make_golden.build_capture(case)
+    frames, pcm, meta = decode_capture(data, FMT_BY_EXT[c['fmt']], system=c['system'])
+    dec = GPUDecoder(system=c['system'], batch=8)
+    dec.set_capture(data, NAME_TO_FMT[c['fmt']])
+    got = []
+    dec.decode(sink=lambda fr, au, m: got.append((fr.copy(), au.copy(), m)))
+    assert len(got) == len(frames) >= 3
+    for (fr, au, m), f, a, om in zip(got, frames, pcm, meta):
+        assert m == om
+        assert np.abs(fr.astype(np.int64) - f.astype(np.int64)).max() <= 1
+        assert np.abs(au.astype(np.int64) - a.astype(np.int64)).max() <= 1
 
 
 def test_gpu_synth_capture_decodes_like_oracle():
