@@ -729,7 +729,14 @@ extern "C" __global__ __launch_bounds__(A1_T) void ldg_k_audio1(
 // Audio phase 2 (lddecode_core.py:335-371): per (read, block, channel) a
 // 16384-point real FFT of the 2.5 MHz audio, bins [0:2048]+[14336:16384]
 // times audio_lpf2, 4096-point IFFT, real part / 4.
-// grid: n_reads * 8 * 2 workgroups of 1024 threads.
+// grid: n_reads * AUDIO2_WG workgroups of 1024 threads: (block j < 4, channel)
+// per read (a read's 2.5 MHz audio, at most MAX_NAUDIO samples, spans first +
+// two middle + last blocks; the static_assert below holds that bound).
+constexpr int AUDIO2_JMAX = 4;
+constexpr int AUDIO2_WG = 2 * AUDIO2_JMAX;
+static_assert((MAX_NAUDIO - 2 * (BLOCKLEN - 64 * AUDIO_DIV2) + (BLOCKLEN - 64 * AUDIO_DIV2) - 1) /
+                          (BLOCKLEN - 64 * AUDIO_DIV2) + 2 <= AUDIO2_JMAX,
+              "audio phase 2: a read needs more blocks than the grid has");
 extern "C" __global__ __launch_bounds__(1024) void ldg_k_audio2(
     const int32_t* __restrict__ smap, const ReadDesc* __restrict__ reads, const double2* __restrict__ tw, const double2* __restrict__ lpf2,
     const double* __restrict__ audio1, int64_t aread_stride, int64_t achan_stride,
@@ -741,8 +748,8 @@ extern "C" __global__ __launch_bounds__(1024) void ldg_k_audio2(
   s_tw[tw_lds_pos(tid)] = tw[2 * tid];
   const TwLds twl{s_tw};
   const int ch = blockIdx.x & 1;
-  const int j = (blockIdx.x >> 1) & 7;
-  const int slot = smap[blockIdx.x >> 4];
+  const int j = (blockIdx.x >> 1) & (AUDIO2_JMAX - 1);
+  const int slot = smap[blockIdx.x / AUDIO2_WG];
   if (status[slot] == FS_EOF) return;
   const ReadDesc rd = reads[slot];
   const int n_in = rd.n_audio, n_out = rd.n_audio2;
