@@ -9,7 +9,7 @@
 // Every output row depends only on its own line and the lines two above and
 // below it (the 2D stencil), with two exceptions that are sequential
 // recurrences: the burst-level EMA `aburstlev` over all lines of all frames
-// (ldg_k_comb_burst, one lane), and FilterIQ's two 1-pole chains per line
+// (ldg_k_comb_burst: speculative chunks, exact), and FilterIQ's two 1-pole chains per line
 // (418 feeds each).  DoYNR's FIR history crosses lines and frames in the
 // reference, but for output pixels (x >= 78) all 25 taps fall inside the same
 // line (h - 12 >= 66 >= 40), so the history never reaches an output pixel.
@@ -154,11 +154,52 @@ using namespace ldg::comb;
 // steps on one lane: ~6k instead of ~30k for a 60-frame call.
 // grid: 1 workgroup of 256 threads.
 constexpr int BURST_PIECE = 40960;   // lines staged per pass (80 KiB of uint16 levels in LDS)
+// raw / IRESCALE correctly rounded from a product and one FMA correction:
+// checked equal to the division for every uint16 (tools/burst_div_check.c)
+__device__ __forceinline__ double burst_level(uint16_t raw) {
+  constexpr double INV = 1.0 / IRESCALE;
+  const double x = (double)raw;
+  const double q = x * INV;
+  return __fma_rn(__fma_rn(-q, IRESCALE, x), INV, q);
+}
 __device__ __forceinline__ double burst_step(double a, uint16_t raw) {
-  const double bk = raw / IRESCALE;                    // comb-ntsc.cxx:560
+  const double bk = burst_level(raw);                  // comb-ntsc.cxx:560
   const double base = (a < 0) ? bk : a;                // :563 (first qualifying line)
   const double e = (base * .99) + (bk * .01);          // :564
   return (bk > 3) ? e : a;
+}
+// The chain over s_u[k0, k1) from state a (abl[k] written when out != null).
+// Once initialised (a > 0) a step is a = (a * m) + c with m = .99, c = bk * .01
+// on a qualifying line and m = 1, c = 0 otherwise -- the same two roundings as
+// the reference, and exactly a again on a skipped line -- so only a multiply and
+// an add are on the dependency path; the levels of 16 lines are computed ahead.
+__device__ __forceinline__ double burst_run(const uint16_t* s_u, int k0, int k1, double a, double* out) {
+  int k = k0;
+  for (; k < k1 && a < 0; k++) {
+    a = burst_step(a, s_u[k]);
+    if (out) out[k] = a;
+  }
+#pragma unroll 1
+  for (; k + 16 <= k1; k += 16) {
+    double m[16], c[16];
+#pragma unroll
+    for (int j = 0; j < 16; j++) {
+      const double bk = burst_level(s_u[k + j]);
+      const bool q = bk > 3;
+      m[j] = q ? .99 : 1.0;
+      c[j] = q ? bk * .01 : 0.0;
+    }
+#pragma unroll
+    for (int j = 0; j < 16; j++) {
+      a = (a * m[j]) + c[j];
+      if (out) out[k + j] = a;
+    }
+  }
+  for (; k < k1; k++) {
+    a = burst_step(a, s_u[k]);
+    if (out) out[k] = a;
+  }
+  return a;
 }
 extern "C" __global__ __launch_bounds__(256) void ldg_k_comb_burst(const uint16_t* __restrict__ frames, int n,
                                                                    double* __restrict__ state,
@@ -184,15 +225,9 @@ extern "C" __global__ __launch_bounds__(256) void ldg_k_comb_burst(const uint16_
     const int c0 = tid * L, c1 = (c0 + L) < cnt ? c0 + L : cnt;
     if (c0 < cnt) {
       const int w = (c0 - warm) > 0 ? c0 - warm : 0;
-      double a = (w == 0) ? a_in : -1.0;
-#pragma unroll 8
-      for (int k = w; k < c0; k++) a = burst_step(a, s_u[k]);
+      double a = burst_run(s_u, w, c0, (w == 0) ? a_in : -1.0, nullptr);
       s_in[tid] = a;
-#pragma unroll 8
-      for (int k = c0; k < c1; k++) {
-        a = burst_step(a, s_u[k]);
-        abl[p0 + k] = a;
-      }
+      a = burst_run(s_u, c0, c1, a, abl + p0);
       s_out[tid] = a;
     }
     __syncthreads();
@@ -203,12 +238,7 @@ extern "C" __global__ __launch_bounds__(256) void ldg_k_comb_burst(const uint16_
     const int last = (cnt - 1) / L;                     // the thread holding the piece's last line
     if (bad < cnt) {
       if (tid == 0) {
-        double a = s_out[bad / L - 1];
-        for (int k = bad; k < cnt; k++) {
-          a = burst_step(a, s_u[k]);
-          abl[p0 + k] = a;
-        }
-        s_out[last] = a;
+        s_out[last] = burst_run(s_u, bad, cnt, s_out[bad / L - 1], abl + p0);
       }
       __syncthreads();
     }
