@@ -55,6 +55,10 @@ def parse():
     ap.add_argument('--cpu-seconds', type=float, default=1.0, help='oracle baseline sample (seconds of RF)')
     ap.add_argument('--no-cpu', action='store_true')
     ap.add_argument('--no-comb', action='store_true', help='stop at .tbc (skip the 2D comb stage)')
+    ap.add_argument('--host-io', action='store_true',
+                    help='PCIe-inclusive (not the headline): each step hands the capture over from host memory '
+                         '(ldg_set_capture) and returns the .tbc frames, audio and rgb48 to host buffers, '
+                         "as lddecode.py's file path does minus the disk (u8 only)")
     ap.add_argument('--prof-all', action='store_true',
                     help='HIP-event timing of every kernel (default: the demod only, the roofline kernel)')
     return ap.parse_args()
@@ -113,7 +117,16 @@ def main():
     synth_s = time.perf_counter() - t0
     progress(rank, 'capture synthesised (%.1f s)' % synth_s)
 
+    host_cap = None
+    if args.host_io:
+        if args.fmt != 0:
+            raise SystemExit('--host-io: u8 captures only')
+        host_cap = dec.ctx.capture_download(0, nsamp)  # the capture in host memory, as a loader would hold it
+
     def step():
+        if host_cap is not None:
+            dec.set_capture(host_cap, args.fmt)         # H2D of the whole capture inside the step
+            return dec.decode(sink=lambda fr, au, meta: None, comb=not args.no_comb, comb_sink=lambda rgb: None)
         dec.use_resident_capture(args.fmt, nsamp)      # fresh read cache: no reuse across steps
         return dec.decode(sink=None, comb=not args.no_comb)
 
@@ -223,7 +236,8 @@ def main():
         'config': {'workload': '%g s NTSC %s, 40 MSPS %s RF per GPU: RF->demod->TBC->.tbc+.pcm%s'
                                % (args.seconds, disc, FMT_NAME[args.fmt], '' if args.no_comb else '->2D comb rgb48'),
                    'frames_per_step': frames // max(args.steps, 1), 'batch_reads': args.batch,
-                   'parallelism': 'capture-sharded x%d' % world},
+                   'parallelism': 'capture-sharded x%d' % world,
+                   'io': 'host buffers over PCIe (--host-io)' if args.host_io else 'HBM-resident'},
         'fields_per_s': round(fields_s, 1), 'realtime_x': round(msps / 40.0, 2),
         'roofline': {'bound': 'hbm', 'kernel': dom_name, 'achieved': round(achieved, 4), 'peak': HBM_PEAK_GBS,
                      'unit': 'GB/s', 'frac': achieved / HBM_PEAK_GBS, 'traffic': traffic,
