@@ -251,7 +251,6 @@ __device__ __forceinline__ double fast_atan2(double y, double x, const double* s
 }
 
 constexpr bool kFastAtan2 = true;
-constexpr int kSkewSleeps = 10;   // the demod's first-wave phase skew (see ldg_k_demod)
 
 struct Pairs {
   double2 a[5], b[5];   // value at k and at M-k of each pair slot
@@ -339,16 +338,6 @@ extern "C" __global__ __launch_bounds__(1024) void ldg_k_demod(
   const int b = blockIdx.x % MAX_BLOCKS_PER_READ;
   const ReadDesc rd = reads[slot];
   if (b >= rd.n_blocks) return;
-  // Phase skew: in a wide launch the first wave of workgroups on odd CUs starts
-  // ~81k cycles (about half a block) late, so the CUs' phases -- the 128 KiB
-  // park store burst, the channel stores -- stop coinciding across the chip for
-  // the rest of the launch.  Interleaved 2-step benches (profiles/r02_s87, s88,
-  // s89 *_skew_ab.txt): 11/11 runs at 89.1-90.2 ms per 60 s decode, against
-  // 89.2-96.4 ms without (5 of 11 runs above 92 ms); ~122k cycles was worse.
-  // Timing only: results are unchanged.
-  if (gridDim.x >= 8 * 256 && blockIdx.x < 256 && (cu_slot() & 1)) {
-    for (int i = 0; i < kSkewSleeps; i++) __builtin_amdgcn_s_sleep(127);   // 127 x 64 cycles each
-  }
 
   const int64_t i0 = rd.s0 + (int64_t)b * BLOCKSTEP;
   const int off = b * BLOCKSTEP;
