@@ -15,7 +15,8 @@ FLAGS = ['--offload-arch=gfx950', '-O3', '-std=c++17', '-fPIC', '-shared',
          # contract a*b+c); FFT butterflies use explicit __fma_rn where they want it.
          '-ffp-contract=off',
          # the machine scheduler's max-ILP strategy (no kernel spills; the demod stays at
-         # 121 VGPRs): bench -1.3% time in 3/3 interleaved rounds, -0.3% in 2/4 (profiles/r02_s84_*, r02_s85_*)
+         # 121 VGPRs): 2-step bench -1.3% time in 3/3 interleaved rounds and -0.3% in 2/4, 20 sustained
+         # steps -0.15% in 2/3 (profiles/r02_s84_*, r02_s85_*, r02_s91_*)
          '-mllvm', '--amdgpu-sched-strategy=max-ilp']
 
 
