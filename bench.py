@@ -48,7 +48,10 @@ def parse():
     ap.add_argument('--steps', type=int, default=2)
     ap.add_argument('--warmup', type=int, default=1)
     ap.add_argument('--seconds', type=float, default=60.0)
-    ap.add_argument('--batch', type=int, default=128)  # with two demod streams 128 measured +1% over 96, 160 slower (tools/batch_ab2.sh)
+    # reads per launch: over the driver's 20 sustained steps 96 beat 128 in 5 of 6 interleaved
+    # comparisons (-0.5..-0.9% time, profiles/r02_s92_s93_batch_20step.txt); in 2-step runs
+    # 128 had measured +1% (tools/batch_ab2.sh), before the clock settles
+    ap.add_argument('--batch', type=int, default=96)
     ap.add_argument('--fmt', type=int, default=0, help='capture format: 0 u8, 1 s16, 2 .r30, 3 .lds (10-bit packed)')
     ap.add_argument('--clv', action='store_true',
                     help='CLV timecode instead of CAV picture numbers (captures past 79,999 frames, e.g. 1 h: config C5)')
