@@ -90,8 +90,12 @@ typedef struct ldg_field_info {
   int32_t linecode_ok[3];           /* 1 = decoded, 0 = None                            */
   int32_t vbi_minutes, vbi_seconds, vbi_clvframe, vbi_framenr, vbi_status, vbi_isclv;
   int32_t burst_group;  /* NTSC burst phase group of the final refine pass */
-  int32_t pad_;
+  int32_t log_flags;    /* what the reference prints while building this Field:
+                         * bit q (q < 16): "vsync vote needed q"    lddecode_core.py:620
+                         * LDG_LOG_NO_VSYNC: "no/corrupt VSYNC found, jumping forward"  :918 */
 } ldg_field_info;
+
+#define LDG_LOG_NO_VSYNC (1 << 16)
 
 typedef struct ldg_ctx ldg_ctx;
 

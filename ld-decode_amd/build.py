@@ -25,11 +25,25 @@ def sources():
         [os.path.join(os.path.dirname(HERE), 'include', 'ldgpu.h'), os.path.abspath(__file__)]
 
 
+STAMP = OUT + '.sha256'      # content hash of the sources + flags the library was built from
+
+
+def source_hash():
+    import hashlib
+    h = hashlib.sha256(' '.join(FLAGS).encode())
+    for s in sources():
+        with open(s, 'rb') as fh:
+            h.update(os.path.basename(s).encode() + b'\0' + fh.read())
+    return h.hexdigest()
+
+
 def up_to_date():
-    if not os.path.exists(OUT):
+    """True when libldgpu.so exists and was built from exactly these sources and flags
+    (content hash, not mtimes: a copied tree keeps its stamp, an edited source does not)."""
+    if not os.path.exists(OUT) or not os.path.exists(STAMP):
         return False
-    t = os.path.getmtime(OUT)
-    return all(os.path.getmtime(s) <= t for s in sources())
+    with open(STAMP) as fh:
+        return fh.read().strip() == source_hash()
 
 
 def build_variant(out, defines=(), verbose=True):
@@ -42,15 +56,21 @@ def build_variant(out, defines=(), verbose=True):
 
 
 def build(force=False, verbose=True):
+    """Compile libldgpu.so unless it is up to date; always says which (the driver's record
+    shows whether this run compiled)."""
     if not force and up_to_date():
         if verbose:
-            print('libldgpu.so up to date')
+            print('libldgpu.so up to date (sources sha256 %s): not recompiled' % source_hash()[:16], flush=True)
         return OUT
     cmd = [HIPCC] + FLAGS + [os.path.join(CSRC, 'ldgpu.hip'), '-o', OUT + '.tmp']
     if verbose:
-        print(' '.join(cmd), flush=True)
+        print('compiling libldgpu.so: ' + ' '.join(cmd), flush=True)
     subprocess.run(cmd, check=True, cwd=CSRC)
     os.replace(OUT + '.tmp', OUT)
+    with open(STAMP, 'w') as fh:
+        fh.write(source_hash() + '\n')
+    if verbose:
+        print('libldgpu.so built (sources sha256 %s)' % source_hash()[:16], flush=True)
     return OUT
 
 

@@ -196,7 +196,7 @@ extern "C" __global__ __launch_bounds__(64) void ldg_k_sync(
   const ReadDesc rd = reads[slot];
   if (lane == 0) R->n_out = rd.n_out;
   if (status[slot] == FS_EOF) {
-    if (lane == 0) { R->status = FS_EOF; R->npeaks = 0; R->nvsync = 0; }
+    if (lane == 0) { R->status = FS_EOF; R->npeaks = 0; R->nvsync = 0; R->log_flags = 0; }
     return;
   }
   const SyncSrc ds(sst, sbits, slot, C);
@@ -373,7 +373,7 @@ extern "C" __global__ __launch_bounds__(64) void ldg_k_sync(
   if (lane == 0) R->npeaks = np;
   for (int k = lane; k < np; k += 64) peaks[(int64_t)slot * MAX_PEAKS + k] = s_pk[k];
   if (overflow) {
-    if (lane == 0) { R->status = FS_CRASH; R->nvsync = 0; }
+    if (lane == 0) { R->status = FS_CRASH; R->nvsync = 0; R->log_flags = 0; }
     return;
   }
   // ---- determine_vsyncs -------------------------------------------------------
@@ -381,7 +381,7 @@ extern "C" __global__ __launch_bounds__(64) void ldg_k_sync(
   int nf = 0;
   double med = 0, tol = 0;
   bool err = false;
-  if (lane == 0) { R->nvsync = 0; R->status = FS_PENDING; }
+  if (lane == 0) { R->nvsync = 0; R->status = FS_PENDING; R->log_flags = 0; }
   int ncand = 0;
   if (np >= 200) {
     // get_hsync_median: the in-range levels in peak order (compacted by ballot)
@@ -466,6 +466,7 @@ extern "C" __global__ __launch_bounds__(64) void ldg_k_sync(
       for (int q = 0; q < nf; q++) {
         if (vs[q][2] == 0) {
           vs[q][1] = -1;
+          R->log_flags |= 1 << q;                     // print("vsync vote needed", i)
           if ((q < nf - 1) && orig[q + 1] != 0) vs[q][2] = -vs[q + 1][2];
           else if ((q >= 1) && orig[q - 1] != 0) vs[q][2] = -vs[q - 1][2];
         }
@@ -489,7 +490,10 @@ extern "C" __global__ __launch_bounds__(64) void ldg_k_sync(
     const int64_t jumpto = V.peak(vs[0][1] - 10, err);
     if (err) { R->status = FS_CRASH; return; }
     R->nextfieldoffset = jumpto;
-    if (jumpto == 0) R->nextfieldoffset = (int64_t)C.linelen * 240;
+    if (jumpto == 0) {
+      R->nextfieldoffset = (int64_t)C.linelen * 240;
+      R->log_flags |= LDG_LOG_NO_VSYNC;               // "no/corrupt VSYNC found, jumping forward"
+    }
     R->status = FS_SHORT;
     return;
   }

@@ -131,6 +131,7 @@ def main(argv=None):
         pcm.write(audio.tobytes())
         meta_all.append(meta)
 
+    dec.frame_log = lambda lines: print('\n'.join(lines))    # the reference's per-field lines
     n = dec.decode(start_frame=firstframe, length=num_frames, sink=sink, comb=args.comb,
                    comb_sink=(lambda r: rgb.write(r.tobytes())) if rgb else None,
                    start_sample=nextsample,

@@ -139,8 +139,41 @@ class GPUField:
         return rec
 
 
+def field_log_lines(fields, ntsc):
+    """The lines the reference prints while reading these fields (in read order), from
+    their status codes and log flags: Field.__init__'s "vsync vote needed i" / "no/corrupt
+    VSYNC found, jumping forward" / 'unable to decode frame' (lddecode_core.py:620,918,939),
+    FieldNTSC's 'not valid' (:1175), the TBC stage's "ERROR: Unable to decode frame,
+    skipping" (:1047,1190), and readframe's `sample nextsample True istop` for every field
+    a readfield call returns (:1263; `sample` is that call's first read position, istop
+    the vsyncs array's 0/1)."""
+    out = []
+    call_start = None
+    for f in fields:
+        if call_start is None:
+            call_start = f.readsample
+        fl = f.info.log_flags
+        for q in range(16):
+            if (fl >> q) & 1:
+                out.append('vsync vote needed %d' % q)
+        if fl & native.LOG_NO_VSYNC:
+            out.append('no/corrupt VSYNC found, jumping forward')
+        st = f.status
+        if st == native.FS_LINELOCS:
+            out.append('unable to decode frame')
+        if ntsc and st in (native.FS_NO_VSYNC, native.FS_SHORT, native.FS_LINELOCS):
+            out.append('not valid')
+        elif st == native.FS_TBC:
+            out.append('ERROR: Unable to decode frame, skipping')
+        if f.valid:
+            out.append('%d %d True %d' % (call_start, f.nextsample, int(f.istop)))
+            call_start = None
+    return out
+
+
 class FrameOut:
-    __slots__ = ('top', 'bottom', 'audio_fields', 'vbi', 'nextsample', 'fields', 'index', 'start', 'tstart', 'mtf0')
+    __slots__ = ('top', 'bottom', 'audio_fields', 'vbi', 'nextsample', 'fields', 'index', 'start', 'tstart', 'mtf0',
+                 'log')
 
     def __init__(self, **kw):
         for k, v in kw.items():
@@ -191,6 +224,7 @@ class GPUDecoder:
         self.transitions = []              # audio-offset chain: linecount of each transition's field
         self.archive, self.arch_next, self.shard_frames = False, 0, []
         self._out_pending = None           # (frames, pics, audio fields, sink) awaiting their audio
+        self.frame_log = None              # callback(lines): the reference's stdout lines of each frame
 
     # ---- capture ---------------------------------------------------------------
     def set_capture(self, data, fmt, device_ptr=None, nsamples=None, first_sample=0, total_bytes=None):
@@ -745,6 +779,7 @@ class GPUDecoder:
                 if keep_from is not None and fr.start < keep_from:
                     continue                    # warm-up frame: chains only
                 fr.fields = [x.record() for x in self.field_log]
+                fr.log = field_log_lines(self.field_log, self.sysp.name == 'NTSC') if self.frame_log else None
                 fr.index = done + len(frames)
                 frames.append(fr)
                 hist = (hist + [x.readsample for x in self.field_log if x.valid])[-16:]
@@ -831,6 +866,8 @@ class GPUDecoder:
             meta = {'frame': fr.index, 'vbi': dict(fr.vbi), 'nextsample': int(fr.nextsample), 'fields': fr.fields}
             self.last_meta = meta
             self.frame_numbers.append(fr.vbi['framenr'])
+            if fr.log:
+                self.frame_log(fr.log)
             if sink:
                 sink(pics[i], audio, meta)
             else:

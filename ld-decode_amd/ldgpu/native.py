@@ -15,6 +15,7 @@ LIB_PATH = os.path.join(HERE, 'libldgpu.so')
 LDG_OK = 0
 FS_VALID, FS_NO_VSYNC, FS_SHORT, FS_LINELOCS, FS_TBC, FS_EOF, FS_CRASH, FS_PENDING = range(8)
 VBI_NONE = -2147483648
+LOG_NO_VSYNC = 1 << 16            # ldg_field_info.log_flags (include/ldgpu.h)
 MAX_VSYNCS = 16
 
 EXPORTS = ['ldg_create', 'ldg_destroy', 'ldg_last_error', 'ldg_set_filters', 'ldg_set_capture',
@@ -33,7 +34,7 @@ class FieldInfo(C.Structure):
                 ('linecode', (C.c_int32 * 6) * 3), ('linecode_ok', C.c_int32 * 3),
                 ('vbi_minutes', C.c_int32), ('vbi_seconds', C.c_int32), ('vbi_clvframe', C.c_int32),
                 ('vbi_framenr', C.c_int32), ('vbi_status', C.c_int32), ('vbi_isclv', C.c_int32),
-                ('burst_group', C.c_int32), ('pad_', C.c_int32)]
+                ('burst_group', C.c_int32), ('log_flags', C.c_int32)]
 
 
 class Config(C.Structure):

@@ -66,14 +66,17 @@ STATUS_CODE = 0x8DC123            # htop 0x8dc -> vbi['status'] (lddecode_core.p
 class FrameCodes:
     """Philips codes per frame: returns the three code words of each field."""
 
-    def __init__(self, first_frame=1, clv=False, fps=30):
+    def __init__(self, first_frame=1, clv=False, fps=30, skip=None):
         self.first, self.clv, self.fps = first_frame, clv, fps
+        self.skip = skip            # (k0, jump): frames k >= k0 are numbered `jump` higher (a cut disc)
 
     def frame_number(self, k):
+        if self.skip is not None and k >= self.skip[0]:
+            return self.first + k + self.skip[1]
         return self.first + k
 
     def codes(self, k):
-        n = self.first + k
+        n = self.frame_number(k)
         if not self.clv:
             c = cav_code(n % 80000)
             return (c, c, STATUS_CODE)
@@ -86,11 +89,12 @@ class SynthRF:
     """Chunked generator.  ``generate(n)`` returns float64 RF; ``encode`` quantises."""
 
     def __init__(self, system='NTSC', first_frame=1, clv=False, seed=20181015, noise=0.02,
-                 start_line=100, audio=True, bars=True, code_fields=(0, 1)):
+                 start_line=100, audio=True, bars=True, code_fields=(0, 1), frame_skip=None, dropouts=()):
         self.p = NTSC if system == 'NTSC' else PAL
         p = self.p
         self.spl = FS * p['line_us'] / 1e6          # samples per line (2542.22 / 2560)
-        self.codes = FrameCodes(first_frame, clv, 30 if system == 'NTSC' else 25)
+        self.codes = FrameCodes(first_frame, clv, 30 if system == 'NTSC' else 25, skip=frame_skip)
+        self.dropouts = tuple(dropouts)              # (first sample, count): RF replaced by noise
         self.seed, self.noise, self.audio = seed, noise, audio
         self.t0_lines = start_line                  # capture starts this many lines into frame 0
         self.bars = bars
@@ -231,6 +235,11 @@ class SynthRF:
         if self.noise:
             rng = np.random.default_rng([self.seed, self.chunk_index])
             rf += rng.normal(0.0, self.noise, count)
+        for d0, dn in self.dropouts:
+            a, b = max(d0, self.pos), min(d0 + dn, self.pos + count)
+            if a < b:           # a dropout: the carrier is lost, only noise remains
+                rng = np.random.default_rng([self.seed, 7, a])
+                rf[a - self.pos:b - self.pos] = rng.normal(0.0, 0.3, b - a)
         self.pos += count
         self.chunk_index += 1
         return rf

@@ -40,3 +40,13 @@ def gpu_ctx_ntsc():
     ctx = native.Context('NTSC', 0, max_reads=8)
     ctx.set_filters(rf.params(), rf.tables)
     return ctx, rf
+
+
+@pytest.fixture(scope='session')
+def gpu_ctx_pal():
+    from ldgpu import native
+    from ldgpu.rfparams import RFTables
+    rf = RFTables('PAL')
+    ctx = native.Context('PAL', 0, max_reads=8)
+    ctx.set_filters(rf.params(), rf.tables)
+    return ctx, rf

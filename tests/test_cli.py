@@ -57,6 +57,44 @@ def test_cli_decode_matches_golden(tmp_path):
     print('CLI: %d/%d frames bit-identical' % (exact, len(frames)))
 
 
+# field reads of this capture start at 0, 1052829, 1721434, ..., 4390767: a 15,000-sample
+# dropout 20,000 samples into the third read breaks both vsync votes of two reads ("vsync vote
+# needed"), one 30,000 samples into the eighth leaves it one vsync ("no/corrupt VSYNC found"),
+# and frame 203 is lost; the first read (mid-field) is 'not valid'
+DROPOUT_CAPTURE = dict(first_frame=200, seed=31, dropouts=((1741434, 15000), (4420767, 15000)))
+
+
+@pytest.mark.gpu
+def test_cli_log_and_invalid_fields_match_oracle(tmp_path):
+    """The CLI's stdout after the argument line is the reference's: per field the
+    Field / FieldNTSC messages and readframe's `sample nextsample True istop`, then
+    `frame N` (lddecode_core.py:620,918,1175,1263; lddecode.py:92) -- on a capture with
+    dropouts that make fields invalid; frames +-1 LSB, audio bit-exact, metadata exact."""
+    import contextlib
+    import io
+    from ldgpu.synth import make_capture
+    from oracle.capture import FMT_U8
+    from oracle.framer import decode_capture
+    data = make_capture(int(40e6 * 0.3), 'u8', **DROPOUT_CAPTURE)
+    buf = io.StringIO()
+    with contextlib.redirect_stdout(buf):
+        frames, pcm, meta = decode_capture(data, FMT_U8, log=print)
+    want = buf.getvalue().splitlines()
+    assert 'vsync vote needed 0' in want and 'no/corrupt VSYNC found, jumping forward' in want
+    cap = tmp_path / 'cap.u8'
+    cap.write_bytes(bytes(data))
+    out = tmp_path / 'out'
+    r = run_cli(cap, out)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert r.stdout.splitlines()[1:] == want
+    got = np.fromfile(str(out) + '.tbc', dtype=np.uint16).reshape(-1, 525 * 910)
+    assert len(got) == len(frames)
+    for g, f in zip(got, frames):
+        assert np.abs(g.astype(np.int64) - f.astype(np.int64)).max() <= 1
+    assert np.array_equal(np.fromfile(str(out) + '.pcm', dtype=np.int16), np.concatenate(pcm))
+    assert json.load(open(str(out) + '.json')) == meta
+
+
 @pytest.mark.gpu
 def test_cli_length_and_comb(tmp_path):
     cap, gold = _golden_capture(tmp_path)
@@ -71,14 +109,68 @@ def test_cli_length_and_comb(tmp_path):
     assert np.abs(o.astype(np.int64) - rgb.astype(np.int64)).max() <= 1
 
 
+def _oracle_findframe(data, target, nextsample=0):
+    """oracle.framer.findframe (lddecode_core.py:1338-1378): (sample, framenr trail, messages)."""
+    from oracle.capture import FMT_U8, Capture
+    from oracle.demod import RFDemod
+    from oracle.framer import findframe
+    logs = []
+    r = findframe(Capture(bytes(data), FMT_U8), RFDemod(system='NTSC'), target, nextsample,
+                  log=lambda *a: logs.append(a))
+    return r, _seek_trail(logs)
+
+
+def _seek_trail(logs):
+    """The VBI frame numbers findframe logs (first loop: (rv, vbi); second loop: (vbi,))
+    and its SEEK messages; the readframe progress lines are ignored."""
+    trail = [a[-1]['framenr'] for a in logs if len(a) in (1, 2) and isinstance(a[-1], dict)]
+    msgs = [a[0] for a in logs if len(a) == 1 and isinstance(a[0], str)]
+    return trail, msgs
+
+
+SEEK_CASES = {
+    # picture numbers on the first field of each frame only: the reference's CAV framing in
+    # findframe (lddecode_core.py:1273-1275) needs a field without one
+    'cav': dict(first_frame=100, seed=11, code_fields=(0,)),
+    # a cut disc: frames from the 16th on are numbered 5 lower (110.. again), so seeking
+    # frame 120 lands on 115 first and needs the retry loop (:1366-1372)
+    'cav_retry': dict(first_frame=100, seed=11, code_fields=(0,), frame_skip=(15, -5)),
+    # frames 115..129 missing: seeking 120 oscillates 135 / 105 and ends in SEEK WARNING (:1375-1376)
+    'cav_warning': dict(first_frame=100, seed=11, code_fields=(0,), frame_skip=(15, 15)),
+    # CLV time codes: tolerance 1 (:1356-1357)
+    'clv': dict(first_frame=5399, seed=12, clv=True),
+}
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('case,target', [('cav', 105), ('cav_retry', 120), ('cav_warning', 120), ('clv', 5405),
+                                         ('clv', 5420)])
+def test_findframe_matches_oracle(case, target):
+    """GPU findframe (ldgpu/decoder.py) against the oracle's restatement of the reference's:
+    the same returned sample, the same trail of VBI frame numbers through the retries, the
+    same SEEK WARNING."""
+    from ldgpu.decoder import GPUDecoder
+    from ldgpu.synth import make_capture
+    data = make_capture(int(40e6 * 1.0), 'u8', **SEEK_CASES[case])
+    want, (trail, msgs) = _oracle_findframe(data, target)
+    dec = GPUDecoder(system='NTSC', batch=8)
+    dec.set_capture(data, 0)
+    logs = []
+    got = dec.findframe(target, 0, log=lambda *a: logs.append(a))
+    assert got == want
+    assert _seek_trail(logs) == (trail, msgs)
+    if case == 'cav_retry':
+        assert trail[-2:] == [115, 120]
+    if case == 'cav_warning':
+        assert msgs == ['SEEK WARNING: seeked to frame 135 instead of 120']
+
+
 @pytest.mark.gpu
 def test_cli_seek_and_cut(tmp_path):
-    """-S seeks by VBI frame number (findframe); -c writes the raw slice between two frames as .r16."""
-    sys.path.insert(0, os.path.join(HERE, 'golden'))
+    """-S seeks by VBI frame number (findframe); -c writes the raw slice between two frames
+    as .r16 (lddecode.py:60-81), with both bounds from the oracle's findframe."""
     from ldgpu.synth import make_capture
-    # picture numbers on the first field of each frame only: the reference's CAV
-    # framing in findframe (lddecode_core.py:1273-1275) needs a field without one
-    data = make_capture(int(40e6 * 0.5), 'u8', first_frame=100, seed=11, code_fields=(0,))
+    data = make_capture(int(40e6 * 0.5), 'u8', **SEEK_CASES['cav'])
     cap = tmp_path / 'cap.u8'
     cap.write_bytes(bytes(data))
     out = tmp_path / 'seek'
@@ -86,17 +178,17 @@ def test_cli_seek_and_cut(tmp_path):
     assert r.returncode == 0, r.stderr[-2000:]
     meta = json.load(open(str(out) + '.json'))
     assert [m['vbi']['framenr'] for m in meta] == [105, 106]
+    first, _ = _oracle_findframe(data, 105)
+    assert meta[0]['fields'][0]['readsample'] == first
     out = tmp_path / 'cut'
     r = run_cli('-c', '-S', 103, '-E', 106, cap, out)
     assert r.returncode == 0, r.stderr[-2000:]
     r16 = np.fromfile(str(out) + '.r16', dtype=np.int16)
-    # the same seek in-process gives the slice bounds (lddecode.py:60-78)
-    from ldgpu.decoder import GPUDecoder
-    dec = GPUDecoder(system='NTSC', batch=8)
-    dec.set_capture(data, 0)
-    spf = dec.rf.samples_per_frame
-    first = dec.findframe(103, 0, log=lambda *a: None)
-    last = dec.findframe(106, first, log=lambda *a: None) + int(spf * .25)
+    from ldgpu.rfparams import RFTables
+    spf = RFTables('NTSC').samples_per_frame          # lddecode.py:41
+    first, _ = _oracle_findframe(data, 103)
+    last, _ = _oracle_findframe(data, 106, first)
+    last += int(spf * .25)
     raw = np.frombuffer(bytes(data), dtype=np.uint8).astype(np.int16)
     assert np.array_equal(r16, raw[first:last])
 

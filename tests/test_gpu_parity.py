@@ -100,33 +100,137 @@ def test_tbc_lines_and_audio(decoded):
         assert nxt[0] == f.audio_next_offset
 
 
-@pytest.mark.parametrize('case', ['ntsc_cav_u8_0p2s', 'ntsc_clv_u8_0p2s', 'ntsc_cav_r30_0p15s',
-                                  'ntsc_cav_lds_0p15s', 'pal_clv_u8_0p2s', 'ntsc_cav_s16_0p15s',
-                                  'ntsc_cav_u8_mid_0p2s'])
-@pytest.mark.parametrize("batch", [3, 16])
-def test_end_to_end_vs_golden(case, batch):
-    """Full decode (speculative batches) vs the oracle's committed golden output."""
+PAL_READS = [(0, 1), (508768, 1), (1311073, 1), (2109792, 1)]   # the PAL golden's reads (+ one sample off)
+
+
+@pytest.fixture(scope='module')
+def decoded_pal(gpu_ctx_pal):
     import sys
     sys.path.insert(0, os.path.join(HERE, 'golden'))
     import make_golden
+    data = make_golden.build_capture('pal_clv_u8_0p2s')
+    ctx, rf = gpu_ctx_pal
+    buf = np.frombuffer(data, np.uint8)
+    ctx.set_capture(buf, buf.size, 0, 0)
+    infos = ctx.decode_reads([r[0] for r in PAL_READS], [r[1] for r in PAL_READS])
+    from oracle.capture import FMT_U8, Capture
+    from oracle.demod import RFDemod
+    from oracle.field import FieldPAL
+    orf = RFDemod(system='PAL')
+    cap = Capture(data, FMT_U8)
+    ref = []
+    for s, m in PAL_READS:
+        raw = orf.demod(cap, s, 1000000, m)
+        ref.append((raw, FieldPAL(orf, raw, 0, audio_offset=0)))
+    return ctx, infos, ref
+
+
+def test_pal_demod_channels(decoded_pal):
+    """PAL demod channels incl. demod_pilot (lddecode_core.py:288-316) within 1e-9 relative."""
+    ctx, infos, ref = decoded_pal
+    for slot, (raw, _) in enumerate(ref):
+        for ci, ch in enumerate(['demod', 'demod_05', 'demod_sync', 'demod_burst', 'demod_pilot']):
+            o = raw[0][ch]
+            g = ctx.debug(slot, ci, np.float64, o.size)
+            assert g.size == o.size
+            scale = max(np.abs(o).max(), 1.0)
+            assert np.abs(g - o).max() / scale < 1e-9, ch
+        for ci, ch in enumerate(['audio_left', 'audio_right']):
+            o = raw[1][ch]
+            g = ctx.debug(slot, 10 + ci, np.float64, o.size)
+            assert np.abs(g - o).max() < 1e-3, ch
+
+
+def test_pal_field_records_and_pilot_refine(decoded_pal):
+    """FieldPAL: peaks, vsyncs, VBI exact; linelocs1/2 and the pilot-refined line locations
+    (refine_linelocs_pilot, lddecode_core.py:962-1021) within 1e-6 samples; the PAL
+    dspicture (lineoffset 3, PAL IRE scaling, :1023-1035) within +-1 LSB; audio within +-1."""
+    ctx, infos, ref = decoded_pal
+    nvalid = 0
+    for slot, (raw, f) in enumerate(ref):
+        inf = infos[slot]
+        assert inf.npeaks == len(f.peaklist)
+        assert np.array_equal(ctx.debug(slot, 41, np.int32, inf.npeaks), np.array(f.peaklist))
+        assert inf.nvsync == len(f.vsyncs)
+        assert inf.nextfieldoffset == f.nextfieldoffset
+        assert (inf.status == 0) == bool(f.valid)
+        if not f.valid:
+            continue
+        nvalid += 1
+        assert inf.istop == int(f.istop) and inf.linecount == f.linecount
+        for q in range(inf.nvsync):
+            assert list(inf.vsync[q]) == [int(x) for x in f.vsyncs[q]]
+        assert inf.vbi_framenr == (f.vbi['framenr'] if f.vbi['framenr'] is not None else -2 ** 31)
+        nl = f.linecount + 4
+        for what, arr in ((20, f.linelocs1), (21, f.linelocs2), (24, f.linelocs)):
+            g = ctx.debug(slot, what, np.float64, nl)
+            assert np.abs(g - np.asarray(arr, dtype=np.float64)).max() < 1e-6, what
+        # the pilot refine moved the lines (the comparison above is not vacuous)
+        assert np.abs(np.asarray(f.linelocs) - np.asarray(f.linelocs2)).max() > 1e-3
+        pic = ctx.debug(slot, 40, np.uint16, f.linecount * 1135)
+        assert pic.size == f.dspicture.size
+        assert np.abs(pic.astype(np.int64) - f.dspicture.astype(np.int64)).max() <= 1
+        pcm, counts, nxt = ctx.field_audio([slot], [0.0])
+        assert counts[0] * 2 == f.dsaudio.size
+        assert np.abs(pcm[0, :2 * counts[0]].astype(np.int64) - f.dsaudio.astype(np.int64)).max() <= 1
+        assert nxt[0] == f.audio_next_offset
+    assert nvalid >= 3
+
+
+CASES = ['ntsc_cav_u8_0p2s', 'ntsc_clv_u8_0p2s', 'ntsc_cav_r30_0p15s', 'ntsc_cav_lds_0p15s', 'pal_clv_u8_0p2s',
+         'ntsc_cav_s16_0p15s', 'ntsc_cav_u8_mid_0p2s']
+_ORACLE = {}
+
+
+def oracle_decode(case):
+    """(capture bytes, golden fixture, oracle frames, pcm, meta) of a golden case, decoded once per
+    session by the oracle; the oracle's output is pinned to the fixture's SHA-256 first."""
+    if case not in _ORACLE:
+        import sys
+        sys.path.insert(0, os.path.join(HERE, 'golden'))
+        import make_golden
+        from oracle.capture import FMT_BY_EXT
+        from oracle.framer import decode_capture
+        with open(os.path.join(HERE, 'golden', case + '.json')) as fh:
+            gold = json.load(fh)
+        c = make_golden.CASES[case]
+        data = make_golden.build_capture(case)
+        assert hashlib.sha256(data).hexdigest() == gold['capture_sha256']
+        frames, pcm, meta = decode_capture(data, FMT_BY_EXT[c['fmt']], system=c['system'])
+        assert len(frames) == len(gold['frames'])
+        for f, a, g in zip(frames, pcm, gold['frames']):
+            assert hashlib.sha256(f.tobytes()).hexdigest() == g['tbc_sha256']
+            assert hashlib.sha256(a.tobytes()).hexdigest() == g['pcm_sha256']
+        _ORACLE[case] = (data, gold, frames, pcm, meta)
+    return _ORACLE[case]
+
+
+@pytest.mark.parametrize('case', CASES)
+@pytest.mark.parametrize("batch", [3, 16])
+def test_end_to_end_vs_golden(case, batch):
+    """Full decode (speculative batches) of every golden case -- NTSC CAV / CLV, PAL CLV, u8 /
+    s16 / .r30 / .lds, a capture starting mid-field -- against the oracle's decode of the same
+    capture (itself pinned to the committed fixture): metadata exact, .tbc within +-1 LSB,
+    .pcm bit-exact (the fixture's SHA-256)."""
     from ldgpu.decoder import GPUDecoder
     from ldgpu.formats import NAME_TO_FMT
-    with open(os.path.join(HERE, 'golden', case + '.json')) as fh:
-        gold = json.load(fh)
-    c = make_golden.CASES[case]
-    data = make_golden.build_capture(case)
+    data, gold, frames, pcm, meta = oracle_decode(case)
+    c = gold['settings']
     dec = GPUDecoder(system=c['system'], batch=batch)
     dec.set_capture(data, NAME_TO_FMT[c['fmt']])
     got = []
     dec.decode(sink=lambda fr, au, meta: got.append((fr.copy(), au.copy(), meta)))
-    assert len(got) == len(gold['frames'])
+    assert len(got) == len(gold['frames']) >= 2
     exact = 0
-    for (fr, au, meta), g in zip(got, gold['frames']):
-        assert meta == g['meta']                     # metadata / VBI / read chain: exact
+    for (fr, au, m), f, a, g in zip(got, frames, pcm, gold['frames']):
+        assert m == g['meta']                        # metadata / VBI / read chain: exact
+        assert fr.size == f.size
+        d = np.abs(fr.astype(np.int64) - f.astype(np.int64))
+        assert d.max() <= 1                          # .tbc: +-1 LSB (north_star)
+        exact += int((d == 0).all())
         assert au.size == g['pcm_len']
-        exact += hashlib.sha256(fr.tobytes()).hexdigest() == g['tbc_sha256']
-    # pixels are checked to +-1 LSB in test_end_to_end_pixels_vs_oracle; report bit-exact frames
-    print('%s batch=%d: %d/%d frames bit-identical to golden' % (case, batch, exact, len(got)))
+        assert hashlib.sha256(au.tobytes()).hexdigest() == g['pcm_sha256']   # .pcm bit-exact
+    print('%s batch=%d: %d/%d frames bit-identical' % (case, batch, exact, len(got)))
 
 
 def test_end_to_end_pixels_vs_oracle(cav_capture):

@@ -1,0 +1,35 @@
+#!/bin/bash
+# One gpurun session, parameterised (replaces the per-session sNN_probe.sh wrappers):
+#   gpurun -- 'bash tools/session.sh TAG STEP [STEP ...]'
+# STEP (each under its own time limit, chained: the first failure ends the session):
+#   tests[=PYTEST-K-EXPR]   pytest -m gpu             -> gpurun_out/TAG_tests.txt
+#   smoke                   __graft_entry__.smoke()   -> gpurun_out/TAG_smoke.txt
+#   bench[=ARGS]            python bench.py ARGS      -> gpurun_out/TAG_bench[N].json (+ .err)
+#   prof[=ARGS]             tools/profile.sh TAG "ARGS" FETCH_SIZE WRITE_SIZE -> gpurun_out/prof/TAG
+#   run=CMD                 any command (bash -c)     -> gpurun_out/TAG_runN.txt
+set -e
+cd "$GRAFT_REPO_ROOT"
+mkdir -p gpurun_out
+TAG=$1; shift
+n=0
+for step in "$@"; do
+  n=$((n+1))
+  name=${step%%=*}; arg=""
+  [[ "$step" == *=* ]] && arg=${step#*=}
+  case $name in
+    tests)
+      k=(); [ -n "$arg" ] && k=(-k "$arg")
+      timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread "${k[@]}" \
+        > gpurun_out/${TAG}_tests.txt 2>&1 ;;
+    smoke)
+      timeout -k 10 180 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/${TAG}_smoke.txt 2>&1 ;;
+    bench)
+      timeout -k 10 600 python bench.py $arg > gpurun_out/${TAG}_bench$n.json 2> gpurun_out/${TAG}_bench$n.err ;;
+    prof)
+      bash tools/profile.sh $TAG "$arg" FETCH_SIZE WRITE_SIZE > gpurun_out/${TAG}_prof.log 2>&1 ;;
+    run)
+      timeout -k 10 600 bash -c "$arg" > gpurun_out/${TAG}_run$n.txt 2>&1 ;;
+    *) echo "unknown step $step"; exit 2 ;;
+  esac
+  echo "step $n ($name) ok"
+done
