@@ -67,6 +67,9 @@ extern "C" {
 #define LDG_FS_EOF 5      /* a block of the read lies beyond the capture window    */
 #define LDG_FS_CRASH 6    /* the reference raises uncaught here (documented)       */
 #define LDG_FS_PENDING 7  /* internal                                               */
+#define LDG_FS_MIGRATED 8 /* the read's demod workgroup moved to another CU mid-block
+                           * (compute-wave save/restore on a shared GPU): its result is
+                           * void, decode the read again                              */
 
 #define LDG_VBI_NONE (-2147483647 - 1) /* Python None in Field.vbi */
 
@@ -133,6 +136,10 @@ typedef struct ldg_filters {
    * recurrences; ldg_set_filters checks fpsync = B/A and fvideoburst
    * (fvideopilot) = fvideo * B/A on every bin and fails with LDG_EINVAL otherwise. */
   const double *iir;
+  /* The 65 taps of F05 (firwin(65, 0.5 MHz), lddecode_core.py:199-202): demod_05 is
+   * rebuilt from the demod channel by this FIR where it is read (no full-rate
+   * channel); ldg_set_filters checks fvideo05 = fvideo * DFT(taps) on every bin. */
+  const double *f05_fir;
 } ldg_filters;
 
 int ldg_create(const ldg_config* cfg, ldg_ctx** out);
@@ -196,7 +203,8 @@ int ldg_assemble_frames(ldg_ctx* ctx, int n, const int32_t* top_slots, const int
 
 /* Debug / parity access to the per-read device arrays of a live slot.
  * what: 0..4 demod channels (demod, demod_05, demod_sync, demod_burst, demod_pilot)
- *       [float64, n_out]; 10,11: audio_left/right after phase 2 [float64];
+ *       [float64, n_out] (demod_05, demod_sync and demod_burst are expanded on request from
+ *       their compact forms); 10,11: audio_left/right after phase 2 [float64];
  *       20..24: linelocs1, linelocs2, linelocs3, linelocs4, final linelocs [float64];
  *       30: burstlevel [float32]; 31: linebad [int8]; 40: dspicture [uint16]; 41: peaklist [int32];
  *       50: the last ldg_comb_ntsc[3d] call's burst-level EMA per line (lines 38..524 of each

@@ -40,6 +40,7 @@ enum FieldStatus {
   FS_EOF = 5,             // a block of this read lies beyond the capture (reference: crash / None)
   FS_CRASH = 6,           // reference would raise uncaught (e.g. vsync within first 11 peaks)
   FS_PENDING = 7,
+  FS_MIGRATED = 8,        // the demod workgroup changed CU mid-block (its park was not private): decode again
 };
 
 // Per-read descriptor, written by the host before a batch.

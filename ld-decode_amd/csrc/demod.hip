@@ -20,6 +20,7 @@
 #include "fft8k.hpp"
 #include "iir.hpp"
 #include "chan.hpp"
+#include "d05.hpp"
 
 using namespace ldg;
 
@@ -319,7 +320,7 @@ extern "C" __global__ __launch_bounds__(1024) void ldg_k_demod(
     double* __restrict__ audio1, int64_t aread_stride, int64_t achan_stride, int32_t* __restrict__ status,
     double2* __restrict__ ospill, SyncTile* __restrict__ stiles, double2* __restrict__ aslice,
     double* __restrict__ sst, uint32_t* __restrict__ sbits, double4* __restrict__ bst,
-    unsigned long long* __restrict__ span) {
+    double* __restrict__ d05halo, unsigned long long* __restrict__ span) {
   __shared__ double2 s_x[M];          // 128 KiB: the 8192-point transforms
   __shared__ uint16_t s_bits[BLOCKLEN / 16];   // sync detector bits
   __shared__ double2 s_tw[TW_LDS_N];           // per-lane FFT twiddles (fft8k.hpp)
@@ -354,7 +355,8 @@ extern "C" __global__ __launch_bounds__(1024) void ldg_k_demod(
   // One park per physical CU (one demod workgroup per CU at a time: 128 KiB of
   // LDS), so consecutive workgroups on a CU rewrite the same 128 KiB and it
   // stays cache-resident instead of streaming 1 GB per launch through HBM.
-  double2* park = ospill + (int64_t)cu_slot() * M;
+  const int my_cu = cu_slot();
+  double2* park = ospill + (int64_t)my_cu * M;
   constexpr double TAU = 6.283185307179586;
 
   // ---- 1. raw samples -> z[m] = x[2m] + i x[2m+1]; forward FFT ---------------
@@ -474,6 +476,11 @@ extern "C" __global__ __launch_bounds__(1024) void ldg_k_demod(
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
   }
+  // The park is private to this CU only while this workgroup stays on it: a
+  // workgroup that compute-wave save/restore resumed on another CU (a shared or
+  // oversubscribed GPU) may have read back a park another workgroup rewrote.
+  // Flag the read: the host decodes it again (FS_MIGRATED).
+  if (tid == 0 && cu_slot() != my_cu) status[slot] = FS_MIGRATED;
   double* ph = reinterpret_cast<double*>(s_x);    // plain (unswizzled) phase scratch
 #pragma unroll
   for (int q = 0; q < 8; q++) ph[tid + T * q] = tho[q];
@@ -528,26 +535,12 @@ extern "C" __global__ __launch_bounds__(1024) void ldg_k_demod(
     pt1 = iir[IIR_P1 + t];
     p151 = iir[IIR_P1 + scan_d15(t & 63)];
     p311 = iir[IIR_P1 + scan_d31(t & 63)];
-    double* o = vout + (int64_t)CH_05 * vchan_stride;
+    // demod_05 itself is not stored (d05.hpp: consumers rebuild the few samples
+    // they read from the video channel); only its sync detector bits are kept
 #pragma unroll
     for (int q = 0; q < 8; q++) {
       const int m = t + T * q;
       const double v0 = zr[q].x * inv, v1 = zr[q].y * inv;
-      // value at block position p lands at rolled position (p - 32) mod 16384 (even: p0 + 1 never wraps)
-      const int p0 = (2 * m - BLOCKCUT_END) & (BLOCKLEN - 1);
-      const bool in0 = p0 >= BLOCKCUT && p0 < BLOCKCUT + copylen;
-      const bool in1 = p0 + 1 >= BLOCKCUT && p0 + 1 < BLOCKCUT + copylen;
-      if (!kProbeNoStore) {
-        // the wave's 64 pairs are all kept or all dropped except at the block ends
-        const int pw0 = (2 * (m & ~63) - BLOCKCUT_END) & (BLOCKLEN - 1);
-        if (pw0 >= BLOCKCUT && pw0 + 127 < BLOCKCUT + copylen) {
-          st_pair(o + p0, make_double2(v0, v1));
-        } else {
-          if (in0 && in1) *reinterpret_cast<double2*>(o + p0) = make_double2(v0, v1);
-          else if (in0) o[p0] = v0;
-          else if (in1) o[p0 + 1] = v1;
-        }
-      }
       // detector bits at UNROLLED block positions 2m, 2m + 1; lanes 8j..8j+7 (pairs
       // of 16 consecutive samples) OR their bits into lane 8j+7 (DPP row shifts)
       const uint32_t f0 = (v0 >= C.sync_lo && v0 <= C.sync_hi) ? 1u : 0u;
@@ -629,6 +622,13 @@ extern "C" __global__ __launch_bounds__(1024) void ldg_k_demod(
   STAMP(18);
   {
     const int t = fresh(tid);
+    if (t < D05_HALO && !kProbeNoStore) {
+      // the video samples demod_05's FIR window needs outside the kept range (d05.hpp):
+      // block positions [992, 1024) and [1024 + copylen, +32) mod 16384
+      const int p = t < 32 ? BLOCKCUT - 32 + t : (BLOCKCUT + copylen + (t - 32)) & (BLOCKLEN - 1);
+      const double2 z = sx[SWC(p >> 1)];
+      d05halo[((int64_t)slot * MAX_BLOCKS_PER_READ + b) * D05_HALO + t] = (p & 1) ? z.y : z.x;
+    }
     double x[IIR_CHUNK];
 #pragma unroll
     for (int c = 0; c < 8; c++) {

@@ -16,6 +16,7 @@
 #include "field_rec.hpp"
 #include "pyops.hpp"
 #include "chan.hpp"
+#include "d05.hpp"
 
 using namespace ldg;
 
@@ -143,7 +144,7 @@ extern "C" __global__ __launch_bounds__(64) void ldg_k_sync_walk(
   const int slot = smap[blockIdx.x / SEG_K];
   const int k = blockIdx.x % SEG_K;
   const int64_t L = (int64_t)slot * SEG_K + k;
-  if (status[slot] == FS_EOF) {
+  if (status[slot] == FS_EOF || status[slot] == FS_MIGRATED) {
     if (lane == 0) node_n[L] = 0;
     return;
   }
@@ -195,8 +196,8 @@ extern "C" __global__ __launch_bounds__(64) void ldg_k_sync(
   FieldRec* R = recs + slot;
   const ReadDesc rd = reads[slot];
   if (lane == 0) R->n_out = rd.n_out;
-  if (status[slot] == FS_EOF) {
-    if (lane == 0) { R->status = FS_EOF; R->npeaks = 0; R->nvsync = 0; R->log_flags = 0; }
+  if (status[slot] == FS_EOF || status[slot] == FS_MIGRATED) {
+    if (lane == 0) { R->status = status[slot]; R->npeaks = 0; R->nvsync = 0; R->log_flags = 0; }
     return;
   }
   const SyncSrc ds(sst, sbits, slot, C);
@@ -707,35 +708,22 @@ extern "C" __global__ __launch_bounds__(64) void ldg_k_linelocs(
 // crossing search and bad-line tests, one wave per line.  Writes the line's
 // refined location to LL2 and its flag to bad[] (0 ok, 1 bad, 2 the reference
 // raises on this line).  grid: n_reads * MAX_LINES workgroups of 64 threads.
-extern "C" __global__ __launch_bounds__(64) void ldg_k_hsync_lines(
-    const int32_t* __restrict__ smap, const double* __restrict__ video, int64_t vread_stride, int64_t vchan_stride, SysConst C,
-    FieldRec* __restrict__ recs, double* __restrict__ lines, int8_t* __restrict__ bad) {
-  prio_latency();
+// demod_05 is not stored (d05.hpp): the wave rebuilds the window of it every
+// test below can touch, [s - 128, s + 576) around the line start s, in LDS;
+// a line whose window leaves the read evaluates the FIR per sample instead.
+namespace {
+constexpr int64_t HS_LO = 128, HS_HI = 576;   // calczc [s-1, s+401]; windows within [s-81, s+522]
 
-  __shared__ double s_tmp[20];
-  const int lane = threadIdx.x;
-  const int slot = smap[blockIdx.x / MAX_LINES];
-  const int i = blockIdx.x % MAX_LINES;
-  FieldRec* R = recs + slot;
-  if (R->status != FS_PENDING) return;
-  if (i >= R->nlines) return;
-  const double* d05 = video + (int64_t)slot * vread_stride + (int64_t)CH_05 * vchan_stride;
-  const int64_t len = R->n_out;
-  const double* L1 = lines + (int64_t)slot * LINES_STRIDE + LL1 * MAX_LINES;
-  double* L2 = lines + (int64_t)slot * LINES_STRIDE + LL2 * MAX_LINES;
-  int8_t* B = bad + (int64_t)slot * MAX_LINES;
+template <class Src>
+__device__ void hsync_line(const Src& d05, int64_t len, const SysConst& C, int i, double v, bool lb, int lane,
+                           double* s_tmp, double& out, int& flag) {
   const double fr = C.freq;
   auto hz = [&](double ire) { return C.ire0 + (C.hz_ire * ire); };
-  auto finish = [&](double v, int flag) {
-    if (lane == 0) { L2[i] = v; B[i] = (int8_t)flag; }
-  };
-  double v = L1[i];
-  bool lb = B[i] != 0;
   if (i < 9) v -= 200;
   const double ll1 = v;
   double zc;
   const int rc = wave_calczc_pf<7>(d05, len, v, hz(-20), 400, lane, &zc);
-  if (rc < 0) { finish(v, 2); return; }
+  if (rc < 0) { out = v; flag = 2; return; }
   if (rc == 0 && !lb) {
     v = zc;
     if (i >= 10) {
@@ -755,7 +743,7 @@ extern "C" __global__ __launch_bounds__(64) void ldg_k_hsync_lines(
       if (grp(ah, bh, hz(-60), hz(20))) isbad = true;
       else if (grp(a1, b1, hz(-60), hz(100))) isbad = true;
       else if (grp(ab, bb, hz(-10), hz(10))) isbad = true;
-      if (raised) { finish(v, 2); return; }
+      if (raised) { out = v; flag = 2; return; }
       if (isbad) {
         lb = true;
       } else {
@@ -772,7 +760,7 @@ extern "C" __global__ __launch_bounds__(64) void ldg_k_hsync_lines(
         const double high = np_mean(s_tmp, (int)(hi - lo));
         double zc2;
         const int rc2 = wave_calczc_pf<3>(d05 + ah, wl, 0, (low + high) / 2, wl, lane, &zc2);
-        if (rc2 != 0) { finish(v, 2); return; }   // None += ... -> TypeError
+        if (rc2 != 0) { out = v; flag = 2; return; }   // None += ... -> TypeError
         zc2 += ((double)py_int(zc) - (fr * 1));
         if (fabs(zc2 - zc) < (fr / 4)) v = zc2;
         else lb = true;
@@ -781,7 +769,44 @@ extern "C" __global__ __launch_bounds__(64) void ldg_k_hsync_lines(
   } else {
     lb = true;
   }
-  finish(v, lb ? 1 : 0);
+  out = v;
+  flag = lb ? 1 : 0;
+}
+}  // namespace
+
+extern "C" __global__ __launch_bounds__(64) void ldg_k_hsync_lines(
+    const int32_t* __restrict__ smap, const ReadDesc* __restrict__ reads, const double* __restrict__ video,
+    int64_t vread_stride, int64_t vchan_stride, SysConst C, FieldRec* __restrict__ recs, double* __restrict__ lines,
+    int8_t* __restrict__ bad, const double* __restrict__ d05halo, const double* __restrict__ f05) {
+  prio_latency();
+
+  __shared__ double s_tmp[20];
+  __shared__ double s_vid[HS_LO + HS_HI + 64];
+  __shared__ double s_d05[HS_LO + HS_HI];
+  const int lane = threadIdx.x;
+  const int slot = smap[blockIdx.x / MAX_LINES];
+  const int i = blockIdx.x % MAX_LINES;
+  FieldRec* R = recs + slot;
+  if (R->status != FS_PENDING) return;
+  if (i >= R->nlines) return;
+  const double* dm = video + (int64_t)slot * vread_stride + (int64_t)CH_DEMOD * vchan_stride;
+  const int64_t len = R->n_out;
+  const D05Src src(dm, d05halo, slot, f05, len, reads[slot].n_blocks);
+  const double* L1 = lines + (int64_t)slot * LINES_STRIDE + LL1 * MAX_LINES;
+  double* L2 = lines + (int64_t)slot * LINES_STRIDE + LL2 * MAX_LINES;
+  int8_t* B = bad + (int64_t)slot * MAX_LINES;
+  const double v = L1[i];
+  const bool lb = B[i] != 0;
+  const int64_t s0 = py_int(i < 9 ? v - 200 : v);
+  double out;
+  int flag;
+  if (s0 - HS_LO >= 0 && s0 + HS_HI <= len) {
+    d05_fill(src, s_vid, s_d05, s0 - HS_LO, s0 + HS_HI, lane);
+    hsync_line(D05Win{s_d05, s0 - HS_LO}, len, C, i, v, lb, lane, s_tmp, out, flag);
+  } else {
+    hsync_line(src, len, C, i, v, lb, lane, s_tmp, out, flag);
+  }
+  if (lane == 0) { L2[i] = out; B[i] = (int8_t)flag; }
 }
 
 // refine_linelocs_hsync, part 2 (per read): bad-line extrapolation and the

@@ -153,7 +153,8 @@ __device__ inline int calczc(const double* data, int64_t len, double start_offse
 
 // ---- one-wave (64 lanes, all calling) versions of the scans above ----------
 // first k in [lo, hi) with data[k] >= target (rising) / <= target, or -1
-__device__ inline int64_t wave_find_first(const double* data, int64_t lo, int64_t hi, bool rising, double target,
+template <class Src>
+__device__ inline int64_t wave_find_first(const Src& data, int64_t lo, int64_t hi, bool rising, double target,
                                           int lane) {
   for (int64_t k0 = lo; k0 < hi; k0 += 64) {
     const int64_t k = k0 + lane;
@@ -166,7 +167,9 @@ __device__ inline int64_t wave_find_first(const double* data, int64_t lo, int64_
 }
 
 // calczc above, wave-parallel search (same result and error semantics)
-__device__ inline int wave_calczc(const double* data, int64_t len, double start_offset, double target, int64_t count,
+// (Src: a pointer, or an indexable source such as d05.hpp's D05Src / D05Win)
+template <class Src>
+__device__ inline int wave_calczc(const Src& data, int64_t len, double start_offset, double target, int64_t count,
                                   int lane, double* res) {
   const int64_t s = py_int(start_offset);
   const int64_t n = count + 1;
@@ -191,8 +194,8 @@ __device__ inline int wave_calczc(const double* data, int64_t len, double start_
 // start, up to 64 * MAXC window samples and their left neighbours), so the
 // search costs one memory latency instead of one per 64-sample chunk.  Windows
 // longer than 64 * MAXC samples, or a negative start, take wave_calczc.
-template <int MAXC>
-__device__ inline int wave_calczc_pf(const double* data, int64_t len, double start_offset, double target,
+template <int MAXC, class Src>
+__device__ inline int wave_calczc_pf(const Src& data, int64_t len, double start_offset, double target,
                                      int64_t count, int lane, double* res) {
   const int64_t s = py_int(start_offset);
   const int64_t n = count + 1;
@@ -245,7 +248,8 @@ __device__ inline double wave_minmax_np(const double* data, int64_t a, int64_t b
 }
 
 // np.min and np.max of data[a, b) (b > a) in one pass (each NaN if any element is NaN)
-__device__ inline void wave_minmax2_np(const double* data, int64_t a, int64_t b, int lane, double& mn, double& mx) {
+template <class Src>
+__device__ inline void wave_minmax2_np(const Src& data, int64_t a, int64_t b, int lane, double& mn, double& mx) {
   double lo = __builtin_inf(), hi = -__builtin_inf();
   bool nan = false;
   for (int64_t k = a + lane; k < b; k += 64) {

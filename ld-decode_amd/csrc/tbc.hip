@@ -17,6 +17,7 @@
 #include "field_rec.hpp"
 #include "pyops.hpp"
 #include "chan.hpp"
+#include "d05.hpp"
 
 using namespace ldg;
 
@@ -742,35 +743,49 @@ __device__ __forceinline__ double* pilot_base(double* scratch, int slot) {
 }
 }  // namespace
 
+// grid: n_reads * MAX_LINES workgroups of 64 threads (one wave per line): the
+// wave rebuilds demod_05 over the window (d05.hpp) and forms the flipped
+// (demod - demod_05) in LDS; lane 0 walks the crossings as the reference does.
 extern "C" __global__ __launch_bounds__(64) void ldg_k_pilot_lines(const int32_t* __restrict__ smap,
+                                                                   const ReadDesc* __restrict__ reads,
                                                                    const double* __restrict__ video,
                                                                    int64_t vread_stride, int64_t vchan_stride,
                                                                    SysConst C, FieldRec* __restrict__ recs,
                                                                    double* __restrict__ lines,
-                                                                   double* __restrict__ scratch) {
+                                                                   double* __restrict__ scratch,
+                                                                   const double* __restrict__ d05halo,
+                                                                   const double* __restrict__ f05) {
   prio_latency();
 
+  constexpr int PW = 256;
+  __shared__ double s_vid[PW + 64];
+  __shared__ double s_d05[PW];
+  __shared__ double s_pil[PW];
   const int lane = threadIdx.x;
-  const int slot = smap[blockIdx.x / LINE_GROUPS];
-  const int grp = blockIdx.x % LINE_GROUPS;
+  const int slot = smap[blockIdx.x / MAX_LINES];
+  const int l = blockIdx.x % MAX_LINES;
   FieldRec* R = recs + slot;
   if (R->status != FS_PENDING) return;
-  const int l = grp * 64 + lane;
   const int nl = R->nlines;
   if (l >= nl) return;
   const double* ll = lines + (int64_t)slot * LINES_STRIDE + LL2 * MAX_LINES;
   const double* dm = video + (int64_t)slot * vread_stride + (int64_t)CH_DEMOD * vchan_stride;
-  const double* d5 = video + (int64_t)slot * vread_stride + (int64_t)CH_05 * vchan_stride;
   const int64_t len = R->n_out;
+  const D05Src d5(dm, d05halo, slot, f05, len, reads[slot].n_blocks);
   double* P = pilot_base(scratch, slot);
   double* offs = P + (int64_t)l * PILOT_MAX;
   double* meta = P + (int64_t)MAX_LINES * PILOT_MAX;    // [count, keep, median] per line
   int64_t a, b;
   py_slice(py_int(ll[l] - 4.7 * C.freq), py_int(ll[l]), len, a, b);
   const int pn = (int)(b > a ? b - a : 0);
-  double pil[256];
-  const int pm = pn < 256 ? pn : 256;
-  for (int i = 0; i < pm; i++) pil[i] = dm[b - 1 - i] - d5[b - 1 - i];   // np.flip
+  const int pm = pn < PW ? pn : PW;
+  if (pm > 0) {
+    d05_fill(d5, s_vid, s_d05, b - pm, b, lane);
+    for (int q = lane; q < pm; q += 64) s_pil[q] = dm[b - 1 - q] - s_d05[pm - 1 - q];   // np.flip
+    __syncthreads();
+  }
+  if (lane != 0) return;
+  const double* pil = s_pil;
   double adjfreq = C.freq;
   if (l > 1) adjfreq /= (ll[l] - ll[l - 1]) / (double)C.linelen;
   int cnt = 0, i = 0;

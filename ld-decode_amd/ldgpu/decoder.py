@@ -457,6 +457,11 @@ class GPUDecoder:
         self.inflight.difference_update(keys)
         import bisect
         for k, sl, inf in zip(keys, slots, infos):
+            if inf.status == native.FS_MIGRATED:
+                # the demod workgroup changed CU mid-block (shared GPU): the read is void and
+                # stays undecoded; the replay's miss decodes it again
+                self.stats['migrated'] = self.stats.get('migrated', 0) + 1
+                continue
             self.cache[k] = (sl, inf)
             if inf.status in (native.FS_VALID, native.FS_SHORT):
                 if k[0] not in self.hints:

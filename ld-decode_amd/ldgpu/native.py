@@ -13,7 +13,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, 'libldgpu.so')
 
 LDG_OK = 0
-FS_VALID, FS_NO_VSYNC, FS_SHORT, FS_LINELOCS, FS_TBC, FS_EOF, FS_CRASH, FS_PENDING = range(8)
+FS_VALID, FS_NO_VSYNC, FS_SHORT, FS_LINELOCS, FS_TBC, FS_EOF, FS_CRASH, FS_PENDING, FS_MIGRATED = range(9)
 VBI_NONE = -2147483648
 LOG_NO_VSYNC = 1 << 16            # ldg_field_info.log_flags (include/ldgpu.h)
 MAX_VSYNCS = 16
@@ -65,7 +65,8 @@ _DP = C.POINTER(C.c_double)
 
 class Filters(C.Structure):
     _fields_ = [(k, _DP) for k in ('rfvideo', 'mtf', 'fvideo', 'fvideo05', 'fvideoburst', 'fvideopilot', 'fpsync',
-                                   'audio_lfilt', 'audio_rfilt', 'audio_lpf2', 'mtf_logabs', 'mtf_arg', 'iir')]
+                                   'audio_lfilt', 'audio_rfilt', 'audio_lpf2', 'mtf_logabs', 'mtf_arg', 'iir',
+                                   'f05_fir')]
 
 
 _lib = None
@@ -210,7 +211,16 @@ class Context:
         info = (FieldInfo * n)()
         self._check(self.lib.ldg_decode_reads(self.h, n, _ptr(s, C.c_int64), _ptr(m), _ptr(sl, C.c_int32), info),
                     'ldg_decode_reads')
-        return list(info)
+        out = list(info)
+        for _ in range(3):
+            # a read whose demod workgroup moved CU mid-block (FS_MIGRATED) is void: decode it again
+            redo = [i for i, x in enumerate(out) if x.status == FS_MIGRATED]
+            if not redo:
+                break
+            again = self.decode_reads(s[redo], m[redo], sl[redo])
+            for i, x in zip(redo, again):
+                out[i] = x
+        return out
 
     def decode_reads_async(self, starts, mtfs, slots):
         """Launch a decode (ldg_decode_reads_async, up to 4 outstanding); decode_reads_wait()

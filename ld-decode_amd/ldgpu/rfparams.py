@@ -96,7 +96,8 @@ class RFTables:
         d0, d1 = S.deemp
         tb, ta = sps.zpk2tf([-d1 * 1e-10], [-d0 * 1e-10], d0 / d1)
         deemp = _whole(sps.bilinear(tb, ta, 1.0 / nyq))
-        f05 = _whole((sps.firwin(65, [0.5 / nyq_mhz], pass_zero=True), [1.0]))
+        f05_fir = sps.firwin(65, [0.5 / nyq_mhz], pass_zero=True)
+        f05 = _whole((f05_fir, [1.0]))
         burst_ba = sps.butter(1, [(S.fsc_mhz - .1) / nyq_mhz, (S.fsc_mhz + .1) / nyq_mhz], btype='bandpass')
         burst = _whole(burst_ba)
         psync_ba = sps.butter(1, 0.05 / nyq_mhz, btype='low')
@@ -118,6 +119,8 @@ class RFTables:
                *burst_ba[0], *burst_ba[1][1:]]
         iir += ([*pilot_ba[0], *pilot_ba[1][1:]] if pilot_ba is not None else [0.0] * 5)
         self.tables['iir'] = np.array(iir, np.float64)
+        # the F05 taps: the library rebuilds demod_05 by this FIR where it is read (csrc/d05.hpp)
+        self.tables['f05_fir'] = np.asarray(f05_fir, np.float64)
 
         # audio (lddecode_core.py:223-279)
         fdiv1 = 32 if inputfreq >= 32 else 16
