@@ -23,7 +23,10 @@ using namespace ldg;
 
 namespace {
 
-constexpr int SPL_MAXN = 2816;                 // max points per line (NTSC ~2545, PAL ~2563)
+constexpr int SPL_MAXN = 2816;                 // whole-line LDS solve up to this many points (NTSC ~2545, PAL ~2563)
+// Longer lines (line locations around a damaged vsync can be 3000+ samples apart) are
+// solved in windows (KTR margin) like the burst pass: any length up to SPL_HARDN.
+constexpr int64_t SPL_HARDN = 1 << 24;
 constexpr int LINE_GROUPS = (MAX_LINES + 63) / 64;
 
 struct CTab { double v[17]; };
@@ -126,7 +129,7 @@ __device__ int spline_block(const Src& buf, int64_t len, double begin, double en
   if (tid < 17) S.ct[tid] = g_ctab.v[tid];
   const int64_t ib = py_int(begin), ie = py_int(end);
   const int64_t n64 = ie - ib;
-  if (ib < 0 || n64 < 6 || n64 >= SPL_MAXN || ib + n64 + 1 > len) return -1;
+  if (ib < 0 || n64 < 6 || n64 >= SPL_HARDN || ib + n64 + 1 > len) return -1;
   const int n = (int)n64;
   const double x0 = begin - (double)ib;
   const double span = end - begin;
@@ -141,7 +144,7 @@ __device__ int spline_block(const Src& buf, int64_t len, double begin, double en
   const int hi = (jhi + 1 + KTR < n - 2) ? jhi + 1 + KTR : n - 2;
   const int base = (lo - 1 < jlo) ? lo - 1 : jlo;            // ys / ms hold j in [base, top]
   const int top = (hi + 1 > jhi + 1) ? hi + 1 : jhi + 1;
-  if (top - base + 1 > SL::cap) return -1;                    // unreachable for n < SPL_MAXN (see callers)
+  if (top - base + 1 > SL::cap) return -2;                    // window larger than the LDS (callers size it)
   double* ys = S.ys - base;
   double* ms = S.ms - base;
   if constexpr (PRELOADED) {
@@ -488,6 +491,33 @@ struct FinalLDS {
   double ra[FINAL_NT / 16], rb[FINAL_NT / 16];
   double m1, mn1;
 };
+// the windowed solve of lines with n >= SPL_MAXN points (shares FinalLDS's memory)
+constexpr int FINAL_WCAP = 1280;
+using FinalWinLDS = SplineLDS<FINAL_NT, FINAL_WCAP>;
+static_assert(sizeof(FinalWinLDS) <= sizeof(FinalLDS), "long-line window must fit the final pass's LDS");
+
+// the demod channel as a spline_block source
+struct ChanSrc {
+  const double* p;
+  __device__ double operator[](int64_t i) const { return p[i]; }
+  __device__ void window(int64_t n0, int64_t n1, double* dst, int tid, int nt) const {
+    for (int64_t i = n0 + tid; i <= n1; i += nt) dst[i - n0] = p[i];
+  }
+};
+
+// .tbc pixel of one resampled value (lddecode_core.py:1139-1142 NTSC, :1030-1035 PAL)
+__device__ __forceinline__ uint16_t tbc_pixel(double v, double wow, const SysConst& C) {
+  const bool pal = C.system == 1;
+  const double scale_ = pal ? (double)(0xd300 - 0x0100) / (100 - C.vsync_ire)
+                            : (double)(0xc800 - 0x0400) / (100 - C.vsync_ire);
+  const double base = pal ? 256.0 : 1024.0;
+  double red = ((v * wow) - C.ire0) / C.hz_ire;           // the reference divides (:1139)
+  red -= C.vsync_ire;
+  double px = (red * scale_) + base;
+  if (px != px) px = 0.0;
+  px = fmin(fmax(px, 0.0), 65535.0) + 0.5;
+  return (uint16_t)px;
+}
 #ifndef LDG_FINAL_WAVES
 #define LDG_FINAL_WAVES 6
 #endif
@@ -497,7 +527,11 @@ extern "C" __global__ __launch_bounds__(FINAL_NT, LDG_FINAL_WAVES) void ldg_k_fi
     SysConst C, FieldRec* __restrict__ recs, const double* __restrict__ lines, const float* __restrict__ blevel,
     uint16_t* __restrict__ pic, int64_t pic_stride) {
   prio_latency();
-  __shared__ FinalLDS S;
+  __shared__ union {
+    FinalLDS S;
+    FinalWinLDS Wn;
+  } U;
+  FinalLDS& S = U.S;
   const int tid = threadIdx.x;
   const int slot = smap[blockIdx.x / MAX_LINES];
   const int row = blockIdx.x % MAX_LINES;
@@ -516,8 +550,34 @@ extern "C" __global__ __launch_bounds__(FINAL_NT, LDG_FINAL_WAVES) void ldg_k_fi
   // ---- geometry (spline_block): y[j] = dm[ib + j], j = 0..n
   const int64_t ib = py_int(begin), ie = py_int(end);
   const int64_t n64 = ie - ib;
-  if (ib < 0 || n64 < 6 || n64 >= SPL_MAXN || ib + n64 + 1 > len) {
+  if (ib < 0 || n64 < 6 || n64 >= SPL_HARDN || ib + n64 + 1 > len) {
     if (tid == 0) R->status = FS_TBC;
+    return;
+  }
+  const bool pal = C.system == 1;
+  if (n64 >= SPL_MAXN) {
+    // a long line: windowed solves over chunks of outputs, each within FINAL_WCAP rows
+    const double wow = (end - begin) / (double)C.linelen;
+    const int64_t oc64 = ((int64_t)(FINAL_WCAP - 2 * KTR - 16) * W) / n64;
+    const int oc = oc64 < 1 ? 1 : (int)oc64;
+    for (int o0 = 0; o0 < W; o0 += oc) {
+      const int o1 = o0 + oc < W ? o0 + oc : W;
+      const int rc = spline_block<FINAL_NT>(ChanSrc{dm}, len, begin, end, W, o0, o1, tid, U.Wn,
+                                            [&](int o, double v) { out[o] = tbc_pixel(v, wow, C); });
+      if (rc < 0) {
+        if (tid == 0) R->status = FS_TBC;
+        return;
+      }
+      __syncthreads();
+    }
+    __syncthreads();
+    if (!pal && tid < 2 && row >= 1 && row < lc - 1) {
+      const float bl = blevel[(int64_t)slot * MAX_LINES + row];
+      const double hzs = 1700000 / 140.0;
+      if (tid == 0) out[0] = bl > 0 ? 16384 : 32768;
+      const double clevel = (1 / 1.45) / hzs;
+      if (tid == 1) out[1] = (uint16_t)(327.67 * clevel * fabs((double)bl));
+    }
     return;
   }
   const int n = (int)n64;
@@ -608,11 +668,6 @@ extern "C" __global__ __launch_bounds__(FINAL_NT, LDG_FINAL_WAVES) void ldg_k_fi
   const double span = end - begin;
   const double step = ((span + x0) - x0) / (double)W;
   const double wow = (end - begin) / (double)C.linelen;
-  const bool pal = C.system == 1;
-  const double scale_ = pal ? (double)(0xd300 - 0x0100) / (100 - C.vsync_ire)
-                            : (double)(0xc800 - 0x0400) / (100 - C.vsync_ire);
-  const double base = pal ? 256.0 : 1024.0;
-  const double rhz = 1.0 / C.hz_ire;
   constexpr int NO = (MAX_OUTW + FINAL_NT - 1) / FINAL_NT;
   double yk[NO], yk1[NO];
   int kk[NO];
@@ -639,12 +694,7 @@ extern "C" __global__ __launch_bounds__(FINAL_NT, LDG_FINAL_WAVES) void ldg_k_fi
     const double a = (double)(k + 1) - x, b = x - (double)k;
     const double m6 = Mk * kSixth, m16 = Mk1 * kSixth;
     const double v = m6 * a * a * a + m16 * b * b * b + (yk[e] - m6) * a + (yk1[e] - m16) * b;
-    double red = ((v * wow) - C.ire0) * rhz;
-    red -= C.vsync_ire;
-    double px = (red * scale_) + base;
-    if (px != px) px = 0.0;
-    px = fmin(fmax(px, 0.0), 65535.0) + 0.5;
-    out[o] = (uint16_t)px;
+    out[o] = tbc_pixel(v, wow, C);
   }
   // NTSC burst flag pixels (threads 0 / 1 wrote pixels 0 / 1 above)
   if (!pal && tid < 2 && row >= 1 && row < lc - 1) {
