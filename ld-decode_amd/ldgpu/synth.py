@@ -32,7 +32,12 @@ NTSC['line_us'] = 227.5 / (NTSC['fsc'] / 1e6)
 PAL = dict(system='PAL', fsc=((1 / 64) * 283.75 + 25 / 1e6) * 1e6, lines=625, ire0=7100000.0, hz_ire=8000.0,
            sync_ire=-.3 * (100 / .7), setup=0.0, burst_ire=21.4, deemp=(100 * .4, 400 * .4),
            audio_l=(1000000 / 64) * 43.75, audio_r=(1000000 / 64) * 68.25,
-           code_lines=((18, 19, 20), (331, 332, 333)), line_us=64.0)
+           code_lines=((18, 19, 20), (331, 332, 333)), line_us=64.0,
+           # the PAL disc's 3.75 MHz pilot on the sync tips (240 cycles per line, so
+           # line-locked), which FieldPAL.refine_linelocs_pilot times the lines by
+           # (lddecode_core.py:962-1021: crossings where demod - demod_05 is in
+           # [-300 kHz, -100 kHz]): 25 IRE = 200 kHz peak deviation
+           pilot_hz=3.75e6, pilot_ire=25.0)
 
 
 def emphasis_filter(sysp):
@@ -157,6 +162,9 @@ class SynthRF:
         ire[broad & (phi < H / 2 - 4.7)] = sync
         nl = normal
         ire[nl & (tau < 4.7)] = sync
+        if p.get('pilot_hz'):
+            tip = ire == sync
+            ire[tip] += p['pilot_ire'] * np.sin(2 * np.pi * p['pilot_hz'] * (t_us[tip] * 1e-6))
         # colour burst: 9 (NTSC) / 10 (PAL) cycles from 5.3 us (5.6 us PAL)
         w = 2 * np.pi * p['fsc'] * (t_us * 1e-6)
         b0 = 5.3 if p['system'] == 'NTSC' else 5.6

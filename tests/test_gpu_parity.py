@@ -100,7 +100,7 @@ def test_tbc_lines_and_audio(decoded):
         assert nxt[0] == f.audio_next_offset
 
 
-PAL_READS = [(0, 1), (508768, 1), (1311073, 1), (2109792, 1)]   # the PAL golden's reads (+ one sample off)
+PAL_READS = [(0, 1), (508767, 1), (1311073, 1), (2109792, 1)]   # the PAL golden's reads (the last one sample off)
 
 
 @pytest.fixture(scope='module')
