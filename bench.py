@@ -36,6 +36,7 @@ FMT_NAME = {0: 'u8', 1: 's16', 2: '10-bit .r30', 3: '10-bit .lds'}
 HBM_PEAK_GBS = 8000.0
 FP64_PEAK_TFLOPS = 78.6                           # MI355X FP64 vector (spec)
 READ_BLOCKS = 66                                  # overlap-save blocks per 1e6-sample field read
+ISO_ITERS = 20                                    # launches of the isolated roofline leg
 # the FFT flops the demod executes per block (5 N log2 N): six 8192-point complex transforms
 # (raw R2C, analytic even / odd, demod R2C, C2R 0.5 MHz, C2R video) + two 1024-point audio IFFTs;
 # sync / burst / pilot are time-domain recurrences (iir.hpp) and are not counted
@@ -164,6 +165,10 @@ def main():
     spans = dec.ctx.profile_spans()        # (launches, total ms) of the demod's execution spans
     busy = dec.ctx.profile_spans_union()   # (launches, ms with at least one demod executing)
     dec.ctx.profile(False)
+    # the roofline leg: the demod alone (kernel ldg_k_demod_iso) over one full-width launch's
+    # reads, ISO_ITERS launches back to back, HIP events on its stream -- the per-dispatch
+    # figure a kernel trace of this command reports for ldg_k_demod_iso (profiles/)
+    iso_reads, iso_ms = dec.demod_isolated(ISO_ITERS)
     reads_timed = dec.stats['reads'] - reads0
     # sanity on the full-size output: consecutive CAV picture numbers, all frames present
     nrs = dec.frame_numbers
@@ -188,47 +193,61 @@ def main():
     disc = 'CLV' if args.clv else 'CAV'
     msps = consumed_all / dt_max / 1e6
     fields_s = 2 * frames_all / dt_max
-    # roofline of the dominant kernel (HIP events around each launch, on the stream it runs on).
-    # The demod is the one kernel that consumes the capture and fills the whole chip (one
-    # 160 KiB-LDS workgroup per CU); the per-read field kernels run concurrently on their own
-    # streams, so summed launch durations overstate them -- the demod is named explicitly.
-    dom_name = 'demod' if 'demod' in stats else (max(stats, key=lambda k: stats[k][1]) if stats else 'demod')
-    dom_launches, dom_ms = stats.get(dom_name, (1, float('nan')))
-    event_ms = dom_ms / max(dom_launches, 1)
-    # the launch duration: the demod's execution span (first workgroup start to last
-    # workgroup end, device constant-rate clock, recorded by the kernel over the timed
-    # region) -- what a kernel trace reports; the HIP-event interval around each launch
-    # on its stream also counts the dispatch's wait for CUs and is reported beside it
-    avg_ms = spans[1] / spans[0] if (dom_name == 'demod' and spans[0]) else event_ms
+    # Roofline of the dominant kernel, the demod (the one kernel that consumes the capture and
+    # fills the chip: one 150 KiB-LDS workgroup per CU).  Unit of work = one RF sample consumed;
+    # algorithmic bytes per unit = SURVEY §8(d): input (1 B u8, 5/4 .lds, 4/3 .r30, 2 s16) +
+    # .tbc out 955,500 / 1,334,667 B + .pcm 0.0048 B (1.7207 B for u8).  One launch of the
+    # roofline leg demodulates `iso_reads` field reads; a read yields consumed / reads_decoded
+    # new samples of the capture (reads overlap by ~1/3 and a few are speculative), so
+    # units per launch = iso_reads * consumed / reads_decoded over the timed steps.
     bps = BYTES_PER_SAMPLE[args.fmt] + NTSC_TBC_BYTES_PER_SAMPLE + NTSC_PCM_BYTES_PER_SAMPLE
-    if not args.no_comb:
-        bps += NTSC_COMB_BYTES_PER_SAMPLE
-    units_per_launch = (consumed / max(args.steps, 1)) / max(dom_launches / max(args.steps, 1), 1)
-    achieved = bps * units_per_launch / (avg_ms * 1e-3) / 1e9
-    # consecutive demod launches alternate between two streams and overlap: a launch's
-    # span includes time it shares with its neighbour.  The demod's own rate is the
-    # time with at least one launch executing, per launch (reported beside the contract figure)
-    busy_ms = busy[1] / busy[0] if (dom_name == 'demod' and busy[0]) else avg_ms
-    achieved_busy = bps * units_per_launch / (busy_ms * 1e-3) / 1e9
-    traffic = None
+    samples_per_read = consumed / max(reads_timed, 1)
+    units_iso = iso_reads * samples_per_read
+    achieved = bps * units_iso / (iso_ms * 1e-3) / 1e9
+    traffic, lds = None, None
     pmc = os.path.join(ROOT, 'profiles', 'pmc_traffic.json')
     if os.path.exists(pmc):
         try:
-            traffic = json.load(open(pmc))['kernels'].get(dom_name)
+            pj = json.load(open(pmc))
+            traffic = pj['kernels'].get('demod_iso')
+            lds = pj.get('demod_iso_sq')
         except Exception:
             traffic = None
-    # secondary bound of the demod kernel: FP64 vector issue (FFT-convention
-    # flops 5 N log2 N: 6 x 8192-point + 2 x 1024-point complex FFTs per block)
-    fp64 = None
-    if 'demod' in stats and stats['demod'][0]:
-        blocks = reads_timed * READ_BLOCKS
-        flops = blocks * DEMOD_FLOPS_PER_BLOCK
-        tf = flops / (stats['demod'][1] * 1e-3) / 1e12
-        tf_busy = flops / (busy[1] * 1e-3) / 1e12 if busy[1] else tf
-        fp64 = {'kernel': 'demod', 'achieved_tflops': round(tf, 3), 'peak_tflops': FP64_PEAK_TFLOPS,
-                'achieved_tflops_busy': round(tf_busy, 3), 'frac_busy': tf_busy / FP64_PEAK_TFLOPS,
-                'frac': tf / FP64_PEAK_TFLOPS, 'flops_per_block': DEMOD_FLOPS_PER_BLOCK,
-                'blocks_per_launch': blocks / stats['demod'][0]}
+    # the pipeline's own demod launches (co-running with the field kernels, two demod streams
+    # overlapping consecutive launches): in-kernel execution spans and HIP-event intervals
+    dom_launches, dom_ms = stats.get('demod', (1, float('nan')))
+    event_ms = dom_ms / max(dom_launches, 1)
+    span_ms = spans[1] / spans[0] if spans[0] else float('nan')
+    busy_ms = busy[1] / busy[0] if busy[0] else float('nan')
+    units_pipe = consumed / max(dom_launches, 1)
+    # secondary bound of the demod: FP64 vector issue (FFT-convention flops 5 N log2 N:
+    # 6 x 8192-point + 2 x 1024-point complex FFTs per block, READ_BLOCKS blocks per read)
+    iso_flops = iso_reads * READ_BLOCKS * DEMOD_FLOPS_PER_BLOCK
+    fp64 = {'achieved_tflops': round(iso_flops / (iso_ms * 1e-3) / 1e12, 3), 'peak_tflops': FP64_PEAK_TFLOPS,
+            'frac': iso_flops / (iso_ms * 1e-3) / 1e12 / FP64_PEAK_TFLOPS,
+            'flops_per_block': DEMOD_FLOPS_PER_BLOCK, 'blocks_per_launch': iso_reads * READ_BLOCKS}
+    roofline = {
+        'bound': 'hbm', 'kernel': 'demod', 'achieved': round(achieved, 4), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
+        'frac': achieved / HBM_PEAK_GBS, 'traffic': traffic,
+        'avg_launch_ms': round(iso_ms, 4),
+        'timing': ('isolated leg: %d launches of ldg_k_demod_iso over %d field reads (%d blocks) back to back, '
+                   'HIP events on its stream; the kernel trace in profiles/ reports ldg_k_demod_iso per dispatch'
+                   % (ISO_ITERS, iso_reads, iso_reads * READ_BLOCKS)),
+        'units_per_launch': round(units_iso), 'algorithmic_bytes_per_sample': round(bps, 4),
+        'algorithmic_bytes_per_launch': round(bps * units_iso),
+        'traffic_unit': 'bytes per launch, 2*FETCH_SIZE + WRITE_SIZE (profiles/pmc_traffic.json, demod_iso)',
+        'traffic_x_algorithmic': (traffic / (bps * units_iso)) if traffic else None,
+        'lds': lds, 'fp64': fp64,
+        'pipeline': {'launches': dom_launches, 'span_ms': round(span_ms, 4), 'hip_event_ms': round(event_ms, 4),
+                     'busy_ms_per_launch': round(busy_ms, 4), 'units_per_launch': round(units_pipe),
+                     'achieved_busy': round(bps * units_pipe / (busy_ms * 1e-3) / 1e9, 4),
+                     'demod_streams': int(os.environ.get('LDG_DEMOD_STREAMS', '2')),
+                     'note': 'the timed steps\' demod launches: in-kernel execution span (device clock), HIP-event '
+                             'interval, and the union of the spans per launch (two demod streams overlap '
+                             'consecutive launches; field kernels co-run on the CUs)'},
+    }
+    if not args.no_comb:
+        roofline['bytes_per_sample_with_comb'] = round(bps + NTSC_COMB_BYTES_PER_SAMPLE, 4)
     cpu = None if args.no_cpu else cpu_baseline(args.cpu_seconds)
     line = {
         'metric': 'RF Msamples/s (40 MSPS NTSC, full RF->.tbc decode)', 'value': round(msps, 3),
@@ -242,17 +261,7 @@ def main():
                    'parallelism': 'capture-sharded x%d' % world,
                    'io': 'host buffers over PCIe (--host-io)' if args.host_io else 'HBM-resident'},
         'fields_per_s': round(fields_s, 1), 'realtime_x': round(msps / 40.0, 2),
-        'roofline': {'bound': 'hbm', 'kernel': dom_name, 'achieved': round(achieved, 4), 'peak': HBM_PEAK_GBS,
-                     'unit': 'GB/s', 'frac': achieved / HBM_PEAK_GBS, 'traffic': traffic,
-                     'avg_launch_ms': round(avg_ms, 4), 'launches': dom_launches,
-                     'timing': 'in-kernel execution span (device wall clock) per launch, HIP-event interval beside it; '
-                               'demod_busy_ms_per_launch: union of the spans (two demod streams overlap launches) / launches',
-                     'hip_event_launch_ms': round(event_ms, 4), 'span_launches': spans[0],
-                     'demod_busy_ms_per_launch': round(busy_ms, 4), 'achieved_busy': round(achieved_busy, 4),
-                     'frac_busy': achieved_busy / HBM_PEAK_GBS,
-                     'demod_streams': int(os.environ.get('LDG_DEMOD_STREAMS', '2')),
-                     'algorithmic_bytes_per_sample': round(bps, 4), 'traffic_unit': 'bytes per launch',
-                     'fp64': fp64},
+        'roofline': roofline,
         'kernels_ms': {k: round(v[1], 3) for k, v in sorted(stats.items(), key=lambda kv: -kv[1][1])},
         'cpu_baseline': cpu,
         'checks': {'framenr_consecutive': consecutive, 'synth_s': round(synth_s, 2),

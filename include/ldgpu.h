@@ -271,6 +271,13 @@ int ldg_profile_spans(ldg_ctx* ctx, double* total_ms, int64_t* count);
  * demod streams overlap consecutive launches) and the launch count. */
 int ldg_profile_spans_union(ldg_ctx* ctx, double* union_ms, int64_t* count);
 
+/* Benchmark roofline leg (not a reference interface): the demod kernel alone
+ * (symbol ldg_k_demod_iso, so a kernel trace separates it from the pipeline's
+ * ldg_k_demod) over n live slots, `iters` launches back to back on one stream;
+ * *ms_per_launch = the mean HIP-event duration of a launch.  The slots' demod
+ * outputs are recomputed in place (a host read cache should be dropped). */
+int ldg_demod_isolated(ldg_ctx* ctx, int n, const int32_t* slots, int iters, double* ms_per_launch);
+
 /* ---- benchmark / test tooling (not a reference interface) ----------------------
  * Synthesise an NTSC LaserDisc RF capture directly into this context's HBM
  * capture buffer (same signal model as ldgpu/synth.py), then make it the

@@ -311,16 +311,21 @@ __device__ unsigned long long g_stamps[LDG_STAMP_BLOCKS][32];
 
 // grid: n_reads * MAX_BLOCKS_PER_READ workgroups of 1024 threads.
 // ospill: PARK_SLOTS x 8192 double2, one odd-half park per physical CU.
-extern "C" __global__ __launch_bounds__(1024) void ldg_k_demod(
-    const int32_t* __restrict__ smap, const ReadDesc* __restrict__ reads, const uint8_t* __restrict__ cap, int64_t cap_first, int64_t cap_nsamp,
-    int fmt, const double2* __restrict__ tw, const double2* __restrict__ twk, const double2* __restrict__ rf_filt,
-    const double2* __restrict__ g_video, const double2* __restrict__ g_05, const double* __restrict__ iir,
-    const double2* __restrict__ a_lfilt, const double2* __restrict__ a_rfilt, SysConst C,
-    double* __restrict__ video, int64_t vread_stride, int64_t vchan_stride,
-    double* __restrict__ audio1, int64_t aread_stride, int64_t achan_stride, int32_t* __restrict__ status,
-    double2* __restrict__ ospill, SyncTile* __restrict__ stiles, double2* __restrict__ aslice,
-    double* __restrict__ sst, uint32_t* __restrict__ sbits, double4* __restrict__ bst,
-    double* __restrict__ d05halo, unsigned long long* __restrict__ span) {
+#define LDG_DEMOD_PARAMS                                                                                          \
+  const int32_t *__restrict__ smap, const ReadDesc *__restrict__ reads, const uint8_t *__restrict__ cap,          \
+      int64_t cap_first, int64_t cap_nsamp, int fmt, const double2 *__restrict__ tw,                             \
+      const double2 *__restrict__ twk, const double2 *__restrict__ rf_filt, const double2 *__restrict__ g_video,  \
+      const double2 *__restrict__ g_05, const double *__restrict__ iir, const double2 *__restrict__ a_lfilt,      \
+      const double2 *__restrict__ a_rfilt, SysConst C, double *__restrict__ video, int64_t vread_stride,          \
+      int64_t vchan_stride, double *__restrict__ audio1, int64_t aread_stride, int64_t achan_stride,              \
+      int32_t *__restrict__ status, double2 *__restrict__ ospill, SyncTile *__restrict__ stiles,                 \
+      double2 *__restrict__ aslice, double *__restrict__ sst, uint32_t *__restrict__ sbits,                      \
+      double4 *__restrict__ bst, double *__restrict__ d05halo, unsigned long long *__restrict__ span
+#define LDG_DEMOD_ARGS                                                                                            \
+  smap, reads, cap, cap_first, cap_nsamp, fmt, tw, twk, rf_filt, g_video, g_05, iir, a_lfilt, a_rfilt, C, video, \
+      vread_stride, vchan_stride, audio1, aread_stride, achan_stride, status, ospill, stiles, aslice, sst, sbits, \
+      bst, d05halo, span
+__device__ __forceinline__ void demod_body(LDG_DEMOD_PARAMS) {
   __shared__ double2 s_x[M];          // 128 KiB: the 8192-point transforms
   __shared__ uint16_t s_bits[BLOCKLEN / 16];   // sync detector bits
   __shared__ double2 s_tw[TW_LDS_N];           // per-lane FFT twiddles (fft8k.hpp)
@@ -660,6 +665,14 @@ extern "C" __global__ __launch_bounds__(1024) void ldg_k_demod(
   STAMP(19);
   if (span && tid == 0) atomicMax(&span[1], (unsigned long long)__builtin_amdgcn_s_memrealtime());
 }
+
+extern "C" __global__ __launch_bounds__(1024) void ldg_k_demod(LDG_DEMOD_PARAMS) { demod_body(LDG_DEMOD_ARGS); }
+
+// The same kernel under its own name for the benchmark's isolated roofline leg
+// (ldg_demod_isolated): its dispatches run alone on the GPU, so a kernel trace's
+// per-dispatch average of this symbol is the figure bench.py measures with HIP
+// events, undisturbed by the field kernels that co-run with ldg_k_demod.
+extern "C" __global__ __launch_bounds__(1024) void ldg_k_demod_iso(LDG_DEMOD_PARAMS) { demod_body(LDG_DEMOD_ARGS); }
 
 // ---------------------------------------------------------------------------
 // Audio phase 1 (lddecode_core.py:321-328): per overlap-save block, the two

@@ -440,6 +440,8 @@ class GPUDecoder:
         self.stats['reads'] += len(keys)
         self.pending.append((keys, slots))
         self.inflight.update(keys)
+        if len(keys) == self.batch:
+            self.wide_slots = list(slots)     # a full-width launch (bench.py's isolated roofline leg)
         return True
 
     def _launch_wait(self):
@@ -483,6 +485,17 @@ class GPUDecoder:
         h = self.stats.setdefault('miss_log', [])
         if len(h) < 64:
             h.append(best)
+
+    def demod_isolated(self, iters=10):
+        """(reads, ms per launch) of the demod alone over the last full-width launch's reads,
+        `iters` launches back to back (the benchmark's roofline leg).  The reads' demod
+        outputs are recomputed in place, so the read cache is dropped."""
+        slots = getattr(self, 'wide_slots', None)
+        if not slots:
+            raise RuntimeError('no full-width launch to time')
+        ms = self.ctx.demod_isolated(slots, iters)
+        self._reset_cache()
+        return len(slots), ms
 
     # ---- reference control flow --------------------------------------------------
     def _get(self, readsample, mtf, audio_offset):

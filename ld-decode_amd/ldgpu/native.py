@@ -21,7 +21,7 @@ MAX_VSYNCS = 16
 EXPORTS = ['ldg_create', 'ldg_destroy', 'ldg_last_error', 'ldg_set_filters', 'ldg_set_capture',
            'ldg_decode_reads', 'ldg_field_audio', 'ldg_assemble_frames', 'ldg_debug_read',
            'ldg_comb_ntsc', 'ldg_comb_reset', 'ldg_version', 'ldg_device_count', 'ldg_profile_enable',
-           'ldg_profile_read', 'ldg_synth_capture', 'ldg_capture_download', 'ldg_comb_ntsc_async', 'ldg_sync',
+           'ldg_profile_read', 'ldg_synth_capture', 'ldg_capture_download', 'ldg_comb_ntsc_async', 'ldg_sync', 'ldg_demod_isolated',
            'ldg_archive_fields', 'ldg_archive_audio', 'ldg_decode_reads_async', 'ldg_decode_reads_wait',
            'ldg_field_audio_async', 'ldg_field_audio_collect', 'ldg_comb_ntsc3d', 'ldg_cx_create', 'ldg_cx_destroy', 'ldg_cx_process', 'ldg_comb_pal', 'ldg_comb_set_state', 'ldg_profile_spans', 'ldg_profile_spans_union']
 
@@ -108,6 +108,7 @@ def load(path=None):
     lib.ldg_archive_fields.argtypes = [vp, C.c_int, vp, C.c_int64]
     lib.ldg_archive_audio.argtypes = [vp, C.c_int, vp, vp, vp, C.c_int64, vp, vp]
     lib.ldg_sync.argtypes = [vp]
+    lib.ldg_demod_isolated.argtypes = [vp, C.c_int, vp, C.c_int, C.POINTER(C.c_double)]
     lib.ldg_profile_enable.argtypes = [vp, C.c_int]
     lib.ldg_profile_read.argtypes = [vp, C.POINTER(KernelStat), C.c_int]
     lib.ldg_profile_spans.argtypes = [vp, C.POINTER(C.c_double), C.POINTER(C.c_int64)]
@@ -346,6 +347,14 @@ class Context:
     def comb_ntsc_async(self, n):
         """ldg_comb_ntsc_async: comb the context's first n device frames on the comb stream."""
         self._check(self.lib.ldg_comb_ntsc_async(self.h, n), 'ldg_comb_ntsc_async')
+
+    def demod_isolated(self, slots, iters):
+        """Mean HIP-event ms of one demod-only launch (ldg_k_demod_iso) over these live slots."""
+        sl = np.ascontiguousarray(slots, dtype=np.int32)
+        ms = C.c_double()
+        self._check(self.lib.ldg_demod_isolated(self.h, sl.size, sl.ctypes.data, iters, C.byref(ms)),
+                    'ldg_demod_isolated')
+        return ms.value
 
     def sync(self):
         self._check(self.lib.ldg_sync(self.h), 'ldg_sync')
