@@ -6,6 +6,7 @@
 #   smoke                   __graft_entry__.smoke()   -> gpurun_out/TAG_smoke.txt
 #   bench[=ARGS]            python bench.py ARGS      -> gpurun_out/TAG_bench[N].json (+ .err)
 #   prof[=ARGS]             tools/profile.sh TAG "ARGS" FETCH_SIZE WRITE_SIZE -> gpurun_out/prof/TAG
+#   sq[=ARGS]               SQ / GRBM counter passes (no trace) -> gpurun_out/prof/TAGsq
 #   run=CMD                 any command (bash -c)     -> gpurun_out/TAG_runN.txt
 set -e
 cd "$GRAFT_REPO_ROOT"
@@ -27,6 +28,12 @@ for step in "$@"; do
       timeout -k 10 600 python bench.py $arg > gpurun_out/${TAG}_bench$n.json 2> gpurun_out/${TAG}_bench$n.err ;;
     prof)
       bash tools/profile.sh $TAG "$arg" FETCH_SIZE WRITE_SIZE > gpurun_out/${TAG}_prof.log 2>&1 ;;
+    sq)
+      # the demod's issue / LDS / FP64 counters (MI355X_MICROARCH.md: <= 8 SQ, 2 GRBM per pass)
+      bash tools/profile.sh ${TAG}sq "$arg" notrace \
+        SQ_WAVE_CYCLES,SQ_BUSY_CYCLES,SQ_WAIT_ANY,SQ_WAIT_INST_ANY,SQ_ACTIVE_INST_ANY,SQ_ACTIVE_INST_LDS,SQ_ACTIVE_INST_VALU,SQ_WAIT_INST_LDS \
+        SQ_INSTS_LDS,SQ_LDS_BANK_CONFLICT,SQ_LDS_IDX_ACTIVE,SQ_INSTS_VALU,SQ_INSTS_VALU_FMA_F64,SQ_INSTS_VALU_MUL_F64,SQ_INSTS_VALU_ADD_F64,SQ_BUSY_CU_CYCLES \
+        GRBM_GUI_ACTIVE,GRBM_COUNT > gpurun_out/${TAG}_sq.log 2>&1 ;;
     run)
       timeout -k 10 600 bash -c "$arg" > gpurun_out/${TAG}_run$n.txt 2>&1 ;;
     *) echo "unknown step $step"; exit 2 ;;
