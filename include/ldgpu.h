@@ -222,6 +222,23 @@ int64_t ldg_debug_read(ldg_ctx* ctx, int slot, int what, void* dst, int64_t cap)
  * NULL keeps the result in the context. */
 int ldg_comb_ntsc(ldg_ctx* ctx, int n, const uint16_t* frames, uint16_t* rgb_out, int io_is_device);
 int ldg_comb_reset(ldg_ctx* ctx);
+/* comb-ntsc's options (main's getopt, comb-ntsc.cxx:972-1091) for every later
+ * ldg_comb_ntsc / ldg_comb_ntsc_async / ldg_comb_ntsc3d call; NULL restores the
+ * defaults.  Values as typed on the reference's command line (IRE, not scaled).
+ * Output frames are 744 x linesout x 3 uint16. */
+typedef struct ldg_comb_opts {
+  double black_ire;    /* -I  setup removed in RGB conversion (default 7.5)          */
+  double brightness;   /* -b  (default 236)                                          */
+  double nr_y;         /* -n  luma noise-reduction clip, IRE (default 1; <= 0 off)   */
+  double nr_c;         /* -N  chroma noise-reduction clip, IRE (default 0 = off)     */
+  int32_t bw;          /* -B  black and white (I = Q = 0)                            */
+  int32_t adaptive2d;  /* 1; -a toggles (Split2D weights fixed at 1)                 */
+  int32_t colorlpf;    /* 1; -L toggles (FilterIQ off)                               */
+  int32_t colorlpf_hq; /* 1; -Q toggles (Q through f_colorlpq)                       */
+  int32_t linesout;    /* 480; -v: 525 (from line 20: the VBI rows; the last 20 black) */
+  int32_t debug_line;  /* -l  line (f_debugline + 25) blacked out; -1000 none        */
+} ldg_comb_opts;
+int ldg_comb_set_opts(ldg_ctx* ctx, const ldg_comb_opts* opts);
 /* Start the comb from a given burst-level EMA (comb-ntsc.cxx:560-566; -1 = not
  * yet initialised, as after ldg_comb_reset): a field-group shard's comb starts
  * from the state the previous shard's frames end in (ldgpu/shard.py). */

@@ -41,16 +41,36 @@ namespace comb {
 
 constexpr int IN_X = 910, IN_Y = 525;
 constexpr int OUT_W = 744, OUT_H = 480, OUT_X0 = 78, FIRST_LINE = 38;
-constexpr int CHAIN_LINES = IN_Y - FIRST_LINE;            // 487 lines feed aburstlev per frame
+constexpr int OUT_HMAX = IN_Y;                             // rows per output frame with -v
+constexpr int ROWS_MAX = IN_Y - 20;                        // combed rows with -v (lines 20..524)
+constexpr int CHAIN_LINES = IN_Y - FIRST_LINE;            // 487 lines feed aburstlev per frame (505 with -v)
+constexpr int CHAIN_MAX = IN_Y - 20;
 constexpr int CV_STRIDE = 912;                             // doubles per row of the cv buffer
-constexpr int IQ_ROW0 = 44 - FIRST_LINE;                   // first output row with FilterIQ (line 44)
-constexpr int IQ_ROWS = OUT_H - IQ_ROW0;                   // 474 rows per frame run the chains
+constexpr int IQ_ROWS_MAX = ROWS_MAX - (44 - 20);          // rows per frame that run the FilterIQ chains
 constexpr double IRESCALE = 358.4, IREBASE = 1024.0;
-constexpr double BLACK_IRE = 7.5, BRIGHTNESS = 236.0;
-constexpr double NR_Y = 1.0 * IRESCALE;
 constexpr double P_2DRANGE = 45 * IRESCALE;
 constexpr double LPI_B0 = 2.267438981796600e-01, LPI_B1 = 2.267438981796600e-01;
 constexpr double LPI_A1 = -5.465122036406802e-01;
+constexpr double LPQ_B0 = 1.169303716013410e-01, LPQ_B1 = 1.169303716013410e-01;   // f_colorlpq (-Q)
+constexpr double LPQ_A1 = -7.661392567973181e-01;
+
+// comb-ntsc's options (main's getopt, comb-ntsc.cxx:972-1091), as the kernels use them
+struct CombOpt {
+  int firstline;      // 38; 20 with -v (linesout == 525): AdjustY / DoYNR / DoCNR / ToRGB start there
+  int nrows;          // combed rows: lines firstline .. firstline + nrows - 1 (480; 505 with -v)
+  int out_rows;       // rows per output frame (linesout); rows >= nrows stay 0 (never written)
+  int adaptive2d;     // Split2D's adaptive weights (-a turns them off)
+  int bw;             // -B: SplitIQ zeroes I and Q
+  int colorlpf;       // FilterIQ (-L turns it off)
+  int lpq;            // -Q: Q through f_colorlpq instead of f_colorlpi
+  int debug_row;      // -l: this output row is black (-1: none)
+  double black_ire;   // -I
+  double bright_m;    // -b: brightness * 256 / 100
+  double nr_y, nr_c;  // -n / -N times irescale; <= 0: DoYNR / DoCNR skipped
+  __host__ __device__ int iq_row0() const { return 44 - firstline; }               // first row with FilterIQ (line 44)
+  __host__ __device__ int iq_rows() const { return nrows - iq_row0(); }
+  __host__ __device__ int chain_lines() const { return IN_Y - firstline; }
+};
 
 struct LP3DTaps { double b[17]; };   // lp_3d = fir1(16, 0.1), comb-ntsc.cxx:379
 __constant__ LP3DTaps g_lp3d = {{0.005719569452904, 0.009426612841315, 0.019748592575455, 0.036822680065252,
@@ -58,6 +78,13 @@ __constant__ LP3DTaps g_lp3d = {{0.005719569452904, 0.009426612841315, 0.0197485
                                  0.124812312996699, 0.119454688318952, 0.104489989820068, 0.082947830292278,
                                  0.058983880135427, 0.036822680065252, 0.019748592575455, 0.009426612841315,
                                  0.005719569452904}};
+struct NRCTaps { double b[17]; };  // deemp.h f_nrc (DoCNR)
+__constant__ NRCTaps g_nrc = {{
+    -3.148569668063267e-03, -4.941974513425438e-03, -9.929538598536455e-03, -1.787793973911701e-02,
+    -2.783702315543740e-02, -3.829928032339736e-02, -4.750186865627083e-02, -5.380281552534787e-02,
+    9.469899799540406e-01,  -5.380281552534787e-02, -4.750186865627083e-02, -3.829928032339737e-02,
+    -2.783702315543740e-02, -1.787793973911701e-02, -9.929538598536455e-03, -4.941974513425442e-03,
+    -3.148569668063267e-03}};
 struct NRTaps { double b[25]; };
 __constant__ NRTaps g_nr = {{
     1.141291975113614e-04, -1.857019211291029e-03, -4.499636864042073e-03, -5.577680979937061e-03,
@@ -73,7 +100,7 @@ __device__ __forceinline__ double clampd(double v, double lo, double hi) { retur
 // clp1 with the three clp0 rows staged in LDS (p = l-2, c = l, n = l+2; the
 // PAL decoder passes l-4 / l+4 and its own p_2drange = 45 * its irescale).
 __device__ __forceinline__ double clp1_lds(const double* p1, const double* c1, const double* n1, int h,
-                                           double p2drange = P_2DRANGE) {
+                                           double p2drange = P_2DRANGE, bool adaptive = true) {
   const double c0 = c1[h], cm = c1[h - 1];
   const double p0 = p1[h], pm = p1[h - 1];
   const double n0 = n1[h], nm = n1[h - 1];
@@ -87,6 +114,7 @@ __device__ __forceinline__ double clp1_lds(const double* p1, const double* c1, c
   kn /= 2;
   kp = clampd(1 - (kp / p2drange), 0, 1);
   kn = clampd(1 - (kn / p2drange), 0, 1);
+  if (!adaptive) kn = kp = 1.0;                          // -a (comb-ntsc.cxx:333)
   double sc = 1.0;
   if (kn != 0 || kp != 0) {
     if (kn > (3 * kp)) kp = 0;
@@ -203,7 +231,8 @@ __device__ __forceinline__ double burst_run(const uint16_t* s_u, int k0, int k1,
 }
 extern "C" __global__ __launch_bounds__(256) void ldg_k_comb_burst(const uint16_t* __restrict__ frames, int n,
                                                                    double* __restrict__ state,
-                                                                   double* __restrict__ abl, int warm) {
+                                                                   double* __restrict__ abl, int warm,
+                                                                   int firstline) {
   prio_latency();
 
   __shared__ uint16_t s_u[BURST_PIECE];
@@ -211,12 +240,13 @@ extern "C" __global__ __launch_bounds__(256) void ldg_k_comb_burst(const uint16_
   __shared__ int s_bad;
   const int tid = threadIdx.x;
   double a_in = state[0];
-  const int total = n * CHAIN_LINES;
+  const int chain = IN_Y - firstline;
+  const int total = n * chain;
   for (int p0 = 0; p0 < total; p0 += BURST_PIECE) {
     const int cnt = (total - p0) < BURST_PIECE ? (total - p0) : BURST_PIECE;
     for (int k = tid; k < cnt; k += 256) {
       const int j = p0 + k;
-      const int f = j / CHAIN_LINES, l = FIRST_LINE + j % CHAIN_LINES;
+      const int f = j / chain, l = firstline + j % chain;
       s_u[k] = frames[(size_t)f * IN_X * IN_Y + (size_t)l * IN_X + 1];
     }
     if (tid == 0) s_bad = cnt;
@@ -249,25 +279,33 @@ extern "C" __global__ __launch_bounds__(256) void ldg_k_comb_burst(const uint16_
 }
 
 // ---- ldg_k_comb_split: SplitIQ's signed chroma of one row.
-// grid: n * 480 workgroups of 256 threads; row r = line r + 38; cv: [n][480][CV_STRIDE].
+// grid: n * O.nrows workgroups of 256 threads; row r = line r + firstline; cv: [n][nrows][CV_STRIDE].
 // D3: frames[f] has its neighbours at frames[f -+ 1] (core / range: p_3dcore,
 // p_3drange times irescale).
 template <bool D3>
 __device__ __forceinline__ void comb_split_row(const uint16_t* __restrict__ frames, double* __restrict__ cvbuf,
-                                               double core, double range) {
+                                               double core, double range, const CombOpt& O) {
   __shared__ uint16_t s_raw[3][IN_X + 2];                // raw lines l-2, l, l+2
   __shared__ double s_c[3][IN_X];                        // Split1D clp0 of those lines
   __shared__ uint16_t s_pn[D3 ? 2 : 1][IN_X + 2];        // 3D: line l of the previous / next frame
   __shared__ double s_x[D3 ? IN_X : 1];                  // 3D: lp_3d's input __k (0 where not fed)
   const int tid = threadIdx.x;
-  const int f = blockIdx.x / OUT_H;
-  const int row = blockIdx.x % OUT_H;
-  const int l = row + FIRST_LINE;
+  const int f = blockIdx.x / O.nrows;
+  const int row = blockIdx.x % O.nrows;
+  const int l = row + O.firstline;
+  double* cvrow = cvbuf + ((size_t)f * O.nrows + row) * CV_STRIDE;
+  if (l < 36 || O.bw) {
+    // SplitIQ covers lines 36..524 (the rest of cbuf is zero); -B zeroes I and Q
+    for (int h = tid; h < CV_STRIDE; h += 256) cvrow[h] = 0.0;
+    return;
+  }
   const uint16_t* fr = frames + (size_t)f * IN_X * IN_Y;
-  // lines are 1820 B apart: 4-byte loads are aligned
+  // lines are 1820 B apart: 4-byte loads are aligned; rows past 524 (l + 2 with -v) are
+  // outside the frame and read as 0 (clpbuffer row 525 is the zeroed next plane)
   for (int t = tid; t < 3 * (IN_X / 2); t += 256) {
     const int k = t / (IN_X / 2), w = t % (IN_X / 2);
-    const uint32_t v = reinterpret_cast<const uint32_t*>(fr + (size_t)(l - 2 + 2 * k) * IN_X)[w];
+    const int r = l - 2 + 2 * k;
+    const uint32_t v = (r < IN_Y) ? reinterpret_cast<const uint32_t*>(fr + (size_t)r * IN_X)[w] : 0u;
     s_raw[k][2 * w] = (uint16_t)(v & 0xffff);
     s_raw[k][2 * w + 1] = (uint16_t)(v >> 16);
   }
@@ -307,7 +345,7 @@ __device__ __forceinline__ void comb_split_row(const uint16_t* __restrict__ fram
   }
   __syncthreads();
   const bool invertphase = (s_raw[1][0] == 16384);
-  double* cvrow = cvbuf + ((size_t)f * OUT_H + row) * CV_STRIDE;
+  const bool adaptive = O.adaptive2d != 0;
   for (int h = tid; h < CV_STRIDE; h += 256) {
     double cv = 0.0;
     if (h >= 4 && h < 840) {
@@ -323,17 +361,17 @@ __device__ __forceinline__ void comb_split_row(const uint16_t* __restrict__ fram
           kk = s_x[h];
         }
         const double k2 = clampd(1 - ((kk - core) / range), 0, 1);
-        const double k1 = 1 - k2;                        // lines 38..517 are all in [2, 523]
+        const double k1 = (l <= 523) ? 1 - k2 : 0.0;     // Split3D :401-403 (Split2D left line 524 at 0)
         const double k0 = 1 - k2 - k1;
         const double clp2 = (double)((((int)s_pn[1][h] + (int)s_pn[0][h]) / 2) - (int)s_raw[1][h]);
-        const double clp1 = (h >= 18) ? clp1_lds(s_c[0], s_c[1], s_c[2], h) : 0.0;
+        const double clp1 = (l < 524 && h >= 18) ? clp1_lds(s_c[0], s_c[1], s_c[2], h, P_2DRANGE, adaptive) : 0.0;
         cavg += clp2 * k2;
         cavg += clp1 * k1;
         cavg += s_c[1][h] * k0;
       } else {
         cavg += 0.0 * 0.0;                               // clpbuffer[2] * combk[2]
         if (l < 524 && h >= 18) {
-          cavg += clp1_lds(s_c[0], s_c[1], s_c[2], h) * 1.0;
+          cavg += clp1_lds(s_c[0], s_c[1], s_c[2], h, P_2DRANGE, adaptive) * 1.0;
           cavg += s_c[1][h] * 0.0;
         } else {
           cavg += 0.0 * 0.0;
@@ -349,31 +387,34 @@ __device__ __forceinline__ void comb_split_row(const uint16_t* __restrict__ fram
 }
 
 extern "C" __global__ __launch_bounds__(256) void ldg_k_comb_split(const uint16_t* __restrict__ frames,
-                                                                   double* __restrict__ cvbuf) {
-  comb_split_row<false>(frames, cvbuf, 0.0, 1.0);
+                                                                   double* __restrict__ cvbuf, CombOpt O) {
+  comb_split_row<false>(frames, cvbuf, 0.0, 1.0, O);
 }
 
 // 3D (-d 3 -F): frames[-1] and frames[n] must be valid (the window's neighbours).
 extern "C" __global__ __launch_bounds__(256) void ldg_k_comb_split3(const uint16_t* __restrict__ frames,
                                                                     double* __restrict__ cvbuf, double core,
-                                                                    double range) {
-  comb_split_row<true>(frames, cvbuf, core, range);
+                                                                    double range, CombOpt O) {
+  comb_split_row<true>(frames, cvbuf, core, range, O);
 }
 
 // ---- ldg_k_comb_iq: FilterIQ's two chains of every row with line >= 44, one
 // lane each.  Feed h: x_h = AdjustY's I (Q) at h = the held value at h + 2;
 // y = ((0 + b0 x_h) + b1 x_{h-2}) - a1 y_prev in the reference's order
-// (Filter::feed, ld-decoder.h:180-186).  grid: ceil(n * 474 * 2 / 256) x 256.
-// iq: [n][474][2][IQ_NS] outputs.
+// (Filter::feed, ld-decoder.h:180-186); Q through f_colorlpq with -Q.
+// grid: ceil(n * iq_rows * 2 / 256) x 256.  iq: [n][iq_rows][2][IQ_NS] outputs.
 extern "C" __global__ __launch_bounds__(256) void ldg_k_comb_iq(const double* __restrict__ cvbuf, int n,
-                                                                double* __restrict__ iq) {
+                                                                double* __restrict__ iq, CombOpt O) {
   prio_latency();
 
+  const int rows = O.iq_rows();
   const int c = blockIdx.x * 256 + threadIdx.x;
-  if (c >= n * IQ_ROWS * 2) return;
-  const int q = c & 1, rr = (c >> 1) % IQ_ROWS, f = (c >> 1) / IQ_ROWS;
-  const double* cv = cvbuf + ((size_t)f * OUT_H + IQ_ROW0 + rr) * CV_STRIDE;
-  double* out = iq + (((size_t)f * IQ_ROWS + rr) * 2 + q) * IQ_NS;
+  if (c >= n * rows * 2) return;
+  const int q = c & 1, rr = (c >> 1) % rows, f = (c >> 1) / rows;
+  const double* cv = cvbuf + ((size_t)f * O.nrows + O.iq_row0() + rr) * CV_STRIDE;
+  double* out = iq + (((size_t)f * rows + rr) * 2 + q) * IQ_NS;
+  const bool lq = q && O.lpq;
+  const double B0 = lq ? LPQ_B0 : LPI_B0, B1 = lq ? LPQ_B1 : LPI_B1, A1 = lq ? LPQ_A1 : LPI_A1;
   // feed k reads the held value at p = H0 + 2k + 2: I (p = 6 + 2k, even) is
   // -cv[p] for even k and +cv[p] for odd k; Q (p = 7 + 2k, odd) is +cv[p] for
   // even k and -cv[p] for odd k; both are 0 at p >= 840 (k = 417).  Lanes c
@@ -394,13 +435,13 @@ extern "C" __global__ __launch_bounds__(256) void ldg_k_comb_iq(const double* __
     for (int j = 0; j < 16; j += 2) {
       if (kb + j < IQ_NS) {
         double ya = 0;
-        ya += (LPI_B0 / 1.0) * xs[j];
-        ya += (LPI_B1 / 1.0) * x1;
-        ya -= (LPI_A1 / 1.0) * y1;
+        ya += (B0 / 1.0) * xs[j];
+        ya += (B1 / 1.0) * x1;
+        ya -= (A1 / 1.0) * y1;
         double yb = 0;
-        yb += (LPI_B0 / 1.0) * xs[j + 1];
-        yb += (LPI_B1 / 1.0) * xs[j];
-        yb -= (LPI_A1 / 1.0) * ya;
+        yb += (B0 / 1.0) * xs[j + 1];
+        yb += (B1 / 1.0) * xs[j];
+        yb -= (A1 / 1.0) * ya;
         x1 = xs[j + 1];
         y1 = yb;
         *reinterpret_cast<double2*>(out + kb + j) = make_double2(ya, yb);
@@ -409,33 +450,59 @@ extern "C" __global__ __launch_bounds__(256) void ldg_k_comb_iq(const double* __
   }
 }
 
-// ---- ldg_k_comb_out: AdjustY, the FilterIQ outputs, DoYNR and ToRGB of one row.
-// grid: n * 480 workgroups of 256 threads.
+// ---- ldg_k_comb_out: AdjustY, the FilterIQ outputs, the VBI copy, DoYNR,
+// DoCNR and ToRGB of one output row.  grid: n * O.out_rows workgroups of 256
+// threads (rows >= O.nrows are the -v frame's never-written bottom rows: 0).
+// For output pixels x >= 78 every FIR tap of DoYNR (h - 12 >= 66 >= 40) and
+// DoCNR (h + 12 - 16 >= 74 >= 60) falls inside the row, so their cross-line
+// histories never reach an output pixel.
 extern "C" __global__ __launch_bounds__(256) void ldg_k_comb_out(const uint16_t* __restrict__ frames,
                                                                  const double* __restrict__ cvbuf,
                                                                  const double* __restrict__ iq,
                                                                  const double* __restrict__ abl,
-                                                                 uint16_t* __restrict__ rgb) {
+                                                                 uint16_t* __restrict__ rgb, CombOpt O) {
   __shared__ uint16_t s_line[IN_X + 2];
-  __shared__ double s_y[IN_X];                           // AdjustY's Y
+  __shared__ uint16_t s_vbi[IN_X + 2];                   // -v: raw line l + 20 (the VBI copy, rows 20..23)
+  __shared__ double s_y[IN_X];                           // AdjustY's Y (+ the VBI copy)
+  __shared__ double s_i[IN_X], s_q[IN_X];                // FilterIQ's I / Q (DoCNR's input)
   const int tid = threadIdx.x;
-  const int f = blockIdx.x / OUT_H;
-  const int row = blockIdx.x % OUT_H;
-  const int l = row + FIRST_LINE;
-  const uint16_t* line = frames + (size_t)f * IN_X * IN_Y + (size_t)l * IN_X;
+  const int f = blockIdx.x / O.out_rows;
+  const int row = blockIdx.x % O.out_rows;
+  uint16_t* out = rgb + ((size_t)f * O.out_rows + row) * OUT_W * 3;
+  if (row >= O.nrows) {
+    for (int x = tid; x < OUT_W * 3; x += 256) out[x] = 0;
+    return;
+  }
+  const int l = row + O.firstline;
+  const uint16_t* fr = frames + (size_t)f * IN_X * IN_Y;
+  const uint16_t* line = fr + (size_t)l * IN_X;
+  const bool vbi = l < 24;                                 // tbuf rows 0..23 hold raw lines 20..43
   for (int w = tid; w < IN_X / 2; w += 256) {
     const uint32_t v = reinterpret_cast<const uint32_t*>(line)[w];
     s_line[2 * w] = (uint16_t)(v & 0xffff);
     s_line[2 * w + 1] = (uint16_t)(v >> 16);
+    if (vbi) {
+      const uint32_t u = reinterpret_cast<const uint32_t*>(fr + (size_t)(l + 20) * IN_X)[w];
+      s_vbi[2 * w] = (uint16_t)(u & 0xffff);
+      s_vbi[2 * w + 1] = (uint16_t)(u >> 16);
+    }
   }
   __syncthreads();
   const bool invertphase = (s_line[0] == 16384);
-  const double* cv = cvbuf + ((size_t)f * OUT_H + row) * CV_STRIDE;
+  const bool ycb = l >= 36;                              // SplitIQ sets cbuf's Y on lines 36..524 only
+  const double* cv = cvbuf + ((size_t)f * O.nrows + row) * CV_STRIDE;
+  const bool fiq = O.colorlpf && l >= 44;
+  const double* iqI = fiq ? iq + (((size_t)f * O.iq_rows() + (row - O.iq_row0())) * 2 + 0) * IQ_NS : nullptr;
+  const double* iqQ = iqI ? iqI + IQ_NS : nullptr;
+  // I / Q at pixel t after FilterIQ (lines >= 44: I from feed (t - 2) / 2, Q from feed
+  // (t - 3) / 2), otherwise AdjustY's I / Q (the held values at t + 2)
+  auto I_at = [&](int t) { return iqI ? iqI[(t - 2) >> 1] : held_i(cv, t + 2); };
+  auto Q_at = [&](int t) { return iqQ ? iqQ[(t - 3) >> 1] : held_q(cv, t + 2); };
   // ---- AdjustY: p[h] = p[h + 2] with y += +-I / +-Q (h in [2, 842)); only
   //      h in [66, 834) reaches an output pixel (DoYNR taps h-12..h+12)
   for (int h = 66 + tid; h < 834; h += 256) {
     const int p = h + 2;
-    const double yy = (p >= 4 && p < 840) ? (double)s_line[p] : 0.0;
+    const double yy = (ycb && p >= 4 && p < 840) ? (double)s_line[p] : 0.0;
     const double ii = held_i(cv, p), qq = held_q(cv, p);
     double comp = 0;
     switch (h & 3) {
@@ -445,37 +512,50 @@ extern "C" __global__ __launch_bounds__(256) void ldg_k_comb_out(const uint16_t*
       default: comp = qq; break;
     }
     if (invertphase) comp = -comp;
-    s_y[h] = yy + comp;
+    s_y[h] = (vbi && h >= 4 && h < 840) ? (double)s_vbi[h] : yy + comp;
+  }
+  if (O.nr_c > 0) {
+    for (int t = 74 + tid; t < 834; t += 256) {
+      s_i[t] = I_at(t);
+      s_q[t] = Q_at(t);
+    }
   }
   __syncthreads();
-  // ---- DoYNR (taps inside this line for x >= 78) + ToRGB
-  const double aburst = abl[(size_t)f * CHAIN_LINES + (l - FIRST_LINE)];
-  const double m = BRIGHTNESS * 256 / 100;
-  const double* iqI = (l >= 44) ? iq + (((size_t)f * IQ_ROWS + (row - IQ_ROW0)) * 2 + 0) * IQ_NS : nullptr;
-  const double* iqQ = iqI ? iqI + IQ_NS : nullptr;
-  uint16_t* out = rgb + ((size_t)f * OUT_H + row) * OUT_W * 3;
+  // ---- DoYNR, DoCNR, ToRGB
+  const double aburst = abl[(size_t)f * O.chain_lines() + (l - O.firstline)];
+  const double m = O.bright_m;
+  const bool black = row == O.debug_row;
   for (int x = tid; x < OUT_W; x += 256) {
     const int h = x + OUT_X0;
-    double y0 = 0;
+    double yv = s_y[h];
+    if (O.nr_y > 0) {
+      double y0 = 0;
 #pragma unroll
-    for (int o = 0; o < 25; o++) y0 += (g_nr.b[o] / 1.0) * s_y[h + 12 - o];
-    double a = y0;
-    if (fabs(a) > NR_Y) a = (a > 0) ? NR_Y : -NR_Y;
-    const double yv = s_y[h] - a;
-    // FilterIQ output at h (lines >= 44): I from feed (h - 2) / 2, Q from feed (h - 3) / 2;
-    // otherwise AdjustY's I / Q (the held values at h + 2)
+      for (int o = 0; o < 25; o++) y0 += (g_nr.b[o] / 1.0) * s_y[h + 12 - o];
+      double a = y0;
+      if (fabs(a) > O.nr_y) a = (a > 0) ? O.nr_y : -O.nr_y;
+      yv = s_y[h] - a;
+    }
     double iv, qv;
-    if (iqI) {
-      iv = iqI[(h - 2) >> 1];
-      qv = iqQ[(h - 3) >> 1];
+    if (O.nr_c > 0) {
+      double ai = 0, aq = 0;
+#pragma unroll
+      for (int o = 0; o < 17; o++) {
+        ai += (g_nrc.b[o] / 1.0) * s_i[h + 12 - o];
+        aq += (g_nrc.b[o] / 1.0) * s_q[h + 12 - o];
+      }
+      if (fabs(ai) > O.nr_c) ai = (ai > 0) ? O.nr_c : -O.nr_c;
+      if (fabs(aq) > O.nr_c) aq = (aq > 0) ? O.nr_c : -O.nr_c;
+      iv = s_i[h] - ai;
+      qv = s_q[h] - aq;
     } else {
-      iv = held_i(cv, h + 2);
-      qv = held_q(cv, h + 2);
+      iv = I_at(h);
+      qv = Q_at(h);
     }
     iv *= (10 / aburst);
     qv *= (10 / aburst);
     double y = u16_to_ire_of(yv);
-    y = (y - BLACK_IRE) * (100 / (100 - BLACK_IRE));
+    y = (y - O.black_ire) * (100 / (100 - O.black_ire));
     const double q = +(iv) / IRESCALE;
     const double i = +(qv) / IRESCALE;
     double r = y + (.956 * i) + (.621 * q);
@@ -484,6 +564,7 @@ extern "C" __global__ __launch_bounds__(256) void ldg_k_comb_out(const uint16_t*
     r = clampd(r * m, 0, 65535);
     g = clampd(g * m, 0, 65535);
     b = clampd(b * m, 0, 65535);
+    if (black) r = g = b = 0;                            // -l: the debug line (comb-ntsc.cxx:586-589)
     out[x * 3 + 0] = (uint16_t)r;
     out[x * 3 + 1] = (uint16_t)g;
     out[x * 3 + 2] = (uint16_t)b;

@@ -50,6 +50,9 @@ def parse(argv=None):
                         'every frame but the first and the last')
     p.add_argument('--comb-3d-core', type=float, default=-1.0, help='comb-ntsc -c (IRE, default 1.25)')
     p.add_argument('--comb-3d-range', type=float, default=-1.0, help='comb-ntsc -r (IRE, default 5.5)')
+    p.add_argument('--comb-args', default='',
+                   help="comb-ntsc options for --comb (NTSC), e.g. '-I 0 -N 1 -v' (comb_ntsc.py's -I -b -n -N "
+                        "-B -a -L -Q -v -l)")
     p.add_argument('--no-json', action='store_true', help='do not write <outfile>.json')
     return p.parse_args(argv)
 
@@ -87,6 +90,15 @@ def main(argv=None):
             print("ERROR: a sharded decode runs the 2D NTSC comb only")
             return 1
     dec = GPUDecoder(system=system, device=args.device, batch=args.batch)
+    if args.comb_args:
+        import shlex
+        import comb_ntsc
+        ca = comb_ntsc.parse(shlex.split(args.comb_args))
+        if isinstance(ca, int) or ca.write8 or ca.pulldown or ca.images or ca.oneframe or ca.dim != 2 or \
+                system != 'NTSC':
+            print("ERROR: --comb-args takes comb-ntsc's arithmetic options (-I -b -n -N -B -a -L -Q -v -l), NTSC")
+            return 1
+        dec.ctx.comb_set_opts(**ca.opts)
     samples_per_frame = dec.rf.samples_per_frame                 # int(fs / FPS) + 1
     bytes_per_frame = samples_per_frame * 5 // 4                 # for 10-bit packed files
     infile_size = os.path.getsize(filename)
@@ -225,9 +237,9 @@ def sharded(args, dec, outname, firstframe, num_frames, nextsample, req_frames, 
         # starts from the state the earlier shards' frames end in (exact, on the host)
         from ldgpu.shard import comb_burst_levels, comb_start_state
         pics = [pic for _, pic, _, _ in res]
-        levels = allgather(comb_burst_levels(pics))
+        levels = allgather(comb_burst_levels(pics, line0=20 if dec.ctx.comb_lines == 525 else 38))
         dec.ctx.comb_set_state(comb_start_state(levels, rank))
-        rgb_bytes = 744 * 480 * 3 * 2
+        rgb_bytes = 744 * dec.ctx.comb_lines * 3 * 2
         with open(outname + '.rgb', 'r+b') as fh:
             fh.seek(first * rgb_bytes)
             for i in range(0, len(pics), dec.ctx.max_frames):

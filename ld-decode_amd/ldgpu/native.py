@@ -21,7 +21,7 @@ MAX_VSYNCS = 16
 EXPORTS = ['ldg_create', 'ldg_destroy', 'ldg_last_error', 'ldg_set_filters', 'ldg_set_capture',
            'ldg_decode_reads', 'ldg_field_audio', 'ldg_assemble_frames', 'ldg_debug_read',
            'ldg_comb_ntsc', 'ldg_comb_reset', 'ldg_version', 'ldg_device_count', 'ldg_profile_enable',
-           'ldg_profile_read', 'ldg_synth_capture', 'ldg_capture_download', 'ldg_comb_ntsc_async', 'ldg_sync', 'ldg_demod_isolated',
+           'ldg_profile_read', 'ldg_synth_capture', 'ldg_capture_download', 'ldg_comb_ntsc_async', 'ldg_sync', 'ldg_demod_isolated', 'ldg_comb_set_opts',
            'ldg_archive_fields', 'ldg_archive_audio', 'ldg_decode_reads_async', 'ldg_decode_reads_wait',
            'ldg_field_audio_async', 'ldg_field_audio_collect', 'ldg_comb_ntsc3d', 'ldg_cx_create', 'ldg_cx_destroy', 'ldg_cx_process', 'ldg_comb_pal', 'ldg_comb_set_state', 'ldg_profile_spans', 'ldg_profile_spans_union']
 
@@ -63,6 +63,17 @@ class SynthParams(C.Structure):
 _DP = C.POINTER(C.c_double)
 
 
+class CombOpts(C.Structure):
+    """ldg_comb_opts (include/ldgpu.h): comb-ntsc's command-line options."""
+    _fields_ = [('black_ire', C.c_double), ('brightness', C.c_double), ('nr_y', C.c_double), ('nr_c', C.c_double),
+                ('bw', C.c_int32), ('adaptive2d', C.c_int32), ('colorlpf', C.c_int32), ('colorlpf_hq', C.c_int32),
+                ('linesout', C.c_int32), ('debug_line', C.c_int32)]
+
+
+COMB_DEFAULTS = dict(black_ire=7.5, brightness=236.0, nr_y=1.0, nr_c=0.0, bw=False, adaptive2d=True, colorlpf=True,
+                     colorlpf_hq=True, linesout=480, debug_line=-1000)
+
+
 class Filters(C.Structure):
     _fields_ = [(k, _DP) for k in ('rfvideo', 'mtf', 'fvideo', 'fvideo05', 'fvideoburst', 'fvideopilot', 'fpsync',
                                    'audio_lfilt', 'audio_rfilt', 'audio_lpf2', 'mtf_logabs', 'mtf_arg', 'iir',
@@ -101,6 +112,7 @@ def load(path=None):
     lib.ldg_debug_read.restype = C.c_int64
     lib.ldg_comb_ntsc.argtypes = [vp, C.c_int, vp, vp, C.c_int]
     lib.ldg_comb_reset.argtypes = [vp]
+    lib.ldg_comb_set_opts.argtypes = [vp, C.POINTER(CombOpts)]
     lib.ldg_comb_ntsc_async.argtypes = [vp, C.c_int]
     lib.ldg_comb_ntsc3d.argtypes = [vp, C.c_int, vp, vp, C.POINTER(C.c_int), C.c_double, C.c_double]
     lib.ldg_decode_reads_async.argtypes = [vp, C.c_int, vp, vp, vp]
@@ -314,7 +326,7 @@ class Context:
         """2D NTSC comb (comb-ntsc.cxx dim=2): n x (525, 910) uint16 frames -> n x (480, 744, 3) rgb48.
         State (burst-level EMA) carries across calls like one reference comb process."""
         f = np.ascontiguousarray(frames, dtype=np.uint16).reshape(-1, 525 * 910)
-        out = np.zeros((f.shape[0], 480, 744, 3), dtype=np.uint16)
+        out = np.zeros((f.shape[0], self.comb_lines, 744, 3), dtype=np.uint16)
         self._check(self.lib.ldg_comb_ntsc(self.h, f.shape[0], f.ctypes.data_as(C.c_void_p),
                                            out.ctypes.data_as(C.c_void_p), 0), 'ldg_comb_ntsc')
         return out
@@ -323,7 +335,7 @@ class Context:
         """3D NTSC comb without optical flow (comb-ntsc -d 3 -F): n x (525, 910) uint16 frames in,
         the rgb48 frames that now have both neighbours out (none for a process's first two frames)."""
         f = np.ascontiguousarray(frames, dtype=np.uint16).reshape(-1, 525 * 910)
-        out = np.zeros((f.shape[0], 480, 744, 3), dtype=np.uint16)
+        out = np.zeros((f.shape[0], self.comb_lines, 744, 3), dtype=np.uint16)
         n_out = C.c_int(0)
         self._check(self.lib.ldg_comb_ntsc3d(self.h, f.shape[0], f.ctypes.data_as(C.c_void_p),
                                              out.ctypes.data_as(C.c_void_p), C.byref(n_out), core_ire, range_ire),
@@ -361,6 +373,20 @@ class Context:
 
     def comb_set_state(self, aburstlev):
         self._check(self.lib.ldg_comb_set_state(self.h, float(aburstlev)), 'ldg_comb_set_state')
+
+    comb_lines = 480                 # rows per rgb48 frame (comb-ntsc -v: 525)
+
+    def comb_set_opts(self, **opts):
+        """comb-ntsc's options (ldg_comb_set_opts; keys of COMB_DEFAULTS, values as on the
+        reference's command line); no arguments restores the defaults."""
+        o = dict(COMB_DEFAULTS)
+        for k, v in opts.items():
+            if k not in o:
+                raise TypeError('unknown comb option %s' % k)
+            o[k] = v
+        c = CombOpts(**{k: (int(v) if isinstance(v, bool) else v) for k, v in o.items()})
+        self._check(self.lib.ldg_comb_set_opts(self.h, C.byref(c)), 'ldg_comb_set_opts')
+        self.comb_lines = int(o['linesout'])
 
     def comb_reset(self):
         self._check(self.lib.ldg_comb_reset(self.h), 'ldg_comb_reset')

@@ -349,17 +349,17 @@ def decode_sharded(dec, rank, world, allgather, sink=None, start_frame=0, length
 COMB_LINE0, COMB_LINES, NTSC_IRESCALE = 38, 525 - 38, 358.4
 
 
-def comb_burst_levels(frames, chunk=64):
+def comb_burst_levels(frames, chunk=64, line0=COMB_LINE0):
     """The burst levels ToRGB reads (comb-ntsc.cxx:560-561: raw[l * 910 + 1] / irescale,
-    lines 38..524), in frame order, for a sequence of 525x910 .tbc frames (a list,
-    an array or a FrameSpill; read `chunk` frames at a time)."""
+    lines line0..524: 38, or 20 with comb-ntsc -v), in frame order, for a sequence of
+    525x910 .tbc frames (a list, an array or a FrameSpill; read `chunk` frames at a time)."""
     if not len(frames):
         return np.zeros(0)
     out = []
     for i in range(0, len(frames), chunk):
         part = frames[i:i + chunk]
         f = np.asarray(part if not isinstance(part, list) else np.stack(part), dtype=np.uint16).reshape(-1, 525, 910)
-        out.append((f[:, COMB_LINE0:525, 1].astype(np.float64) / NTSC_IRESCALE).reshape(-1))
+        out.append((f[:, line0:525, 1].astype(np.float64) / NTSC_IRESCALE).reshape(-1))
     return np.concatenate(out)
 
 

@@ -20,6 +20,8 @@ def _load():
     lib.comb2d_create.restype = C.c_void_p
     lib.comb2d_destroy.argtypes = [C.c_void_p]
     lib.comb2d_process.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p]
+    lib.comb2d_set_opts.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
+    lib.comb3d_set_opts.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
     lib.comb2d_aburstlev.argtypes = [C.c_void_p]
     lib.comb2d_aburstlev.restype = C.c_double
     lib.comb3d_create.restype = C.c_void_p
@@ -31,12 +33,33 @@ def _load():
     return lib
 
 
-class Comb2D:
-    """One reference comb process: state (aburstlev, Y-NR FIR history) carries across calls."""
+DEFAULT_OPTS = dict(black_ire=7.5, brightness=236.0, nr_y=1.0, nr_c=0.0, bw=False, adaptive2d=True,
+                    colorlpf=True, colorlpf_hq=True, linesout=480, debugline=-1000)
 
-    def __init__(self):
+
+def _set_opts(fn, h, opts):
+    """comb-ntsc's options (comb-ntsc.cxx:972-1091): -I black_ire, -b brightness, -n nr_y,
+    -N nr_c (IRE), -B bw, -a / -L / -Q toggles, -v linesout 525, -l debugline."""
+    o = dict(DEFAULT_OPTS)
+    for k, v in opts.items():
+        if k not in o:
+            raise TypeError('unknown comb option %s' % k)
+        o[k] = v
+    d = np.array([o['black_ire'], o['brightness'], o['nr_y'], o['nr_c']], dtype=np.float64)
+    i = np.array([o['bw'], o['adaptive2d'], o['colorlpf'], o['colorlpf_hq'], o['linesout'], o['debugline']],
+                 dtype=np.int32)
+    fn(h, d.ctypes.data, i.ctypes.data)
+    return o
+
+
+class Comb2D:
+    """One reference comb process: state (aburstlev, Y-NR / C-NR FIR histories) carries
+    across calls.  Keyword options as in DEFAULT_OPTS (comb-ntsc's command line)."""
+
+    def __init__(self, **opts):
         self.lib = _load()
         self.h = self.lib.comb2d_create()
+        self.opts = _set_opts(self.lib.comb2d_set_opts, self.h, opts)
 
     def __del__(self):
         if getattr(self, 'h', None):
@@ -45,7 +68,7 @@ class Comb2D:
 
     def process(self, frames):
         f = np.ascontiguousarray(frames, dtype=np.uint16).reshape(-1, IN_Y, IN_X)
-        out = np.zeros((f.shape[0], OUT_H, OUT_W, 3), dtype=np.uint16)
+        out = np.zeros((f.shape[0], self.opts['linesout'], OUT_W, 3), dtype=np.uint16)
         self.lib.comb2d_process(self.h, f.shape[0], f.ctypes.data, out.ctypes.data)
         return out
 
@@ -58,10 +81,11 @@ class Comb3D:
     """One reference comb process run as `comb-ntsc -d 3 -F [-c core] [-r range]`:
     frame k is output once frame k+1 has arrived (none for the first two inputs)."""
 
-    def __init__(self, core_ire=-1.0, range_ire=-1.0):
+    def __init__(self, core_ire=-1.0, range_ire=-1.0, **opts):
         self.lib = _load()
         self.h = self.lib.comb3d_create()
         self.core, self.range = core_ire, range_ire
+        self.opts = _set_opts(self.lib.comb3d_set_opts, self.h, opts)
 
     def __del__(self):
         if getattr(self, 'h', None):
@@ -70,7 +94,7 @@ class Comb3D:
 
     def process(self, frames):
         f = np.ascontiguousarray(frames, dtype=np.uint16).reshape(-1, IN_Y, IN_X)
-        out = np.zeros((f.shape[0], OUT_H, OUT_W, 3), dtype=np.uint16)
+        out = np.zeros((f.shape[0], self.opts['linesout'], OUT_W, 3), dtype=np.uint16)
         n = self.lib.comb3d_process(self.h, f.shape[0], f.ctypes.data, out.ctypes.data, self.core, self.range)
         return out[:n]
 

@@ -16,7 +16,7 @@
 //   FilterIQ                        :212-243   (fresh colorlpi IIR per line, HQ)
 //   VBI copy                        :870-877
 //   DoYNR                           :523-553   (persistent f_nr FIR across lines + frames)
-//   DoCNR                           :485-521   (nr_c = 0: no-op)
+//   DoCNR                           :485-521   (persistent f_nrc FIRs on I and Q, -N)
 //   ToRGB / RGB::conv / u16_to_ire  :555-598, :124-147, :116-121
 //   PostProcess + WriteFrame        :894-938, :704-733 (rows 38..517, x 78..821)
 //   3D (-d 3 -F): Process with f = 1 :837,851-866 (no output for the first two
@@ -27,7 +27,11 @@
 //   Build-defined (parity unpinned): Split3D reads _k[4] and _k[832..835],
 //   which it never writes (uninitialised stack in the reference); here 0.
 //   Filter::feed (DF-I order)       ld-decoder.h:167-214
-//   f_nr, f_colorlpi constants      deemp.h:367-380, :425-432
+//   f_nr, f_nrc, f_colorlpi/q       deemp.h:367-380, :412-423, :425-441
+// Options (main's getopt, comb-ntsc.cxx:972-1091), struct Opts: -I black_ire,
+// -b brightness, -n nr_y, -N nr_c, -B b&w, -a (adaptive 2D off), -L (no colour
+// LPF), -Q (Q through colorlpq), -v (linesout 525: firstline 20, the VBI copy
+// shows), -l (debug line blacked out).  Output frames are 744 x linesout.
 #include <cmath>
 #include <cstdint>
 #include <algorithm>
@@ -38,10 +42,8 @@
 namespace {
 
 constexpr int IN_X = 910, IN_Y = 525;
-constexpr int OUT_W = 744, OUT_H = 480, OUT_X0 = 78, FIRST_LINE = 38;
+constexpr int OUT_W = 744, OUT_X0 = 78;
 constexpr double IRESCALE = 358.4, IREBASE = 1024.0;
-constexpr double BLACK_IRE = 7.5, BRIGHTNESS = 236.0;
-constexpr double NR_Y = 1.0 * IRESCALE;      // main(): nr_y *= irescale
 constexpr double P_2DRANGE = 45 * IRESCALE;  // Split2D sets it per pixel
 
 // deemp.h f_nr (25-tap high pass used by DoYNR)
@@ -59,9 +61,24 @@ const double LP3D_B[17] = {0.005719569452904, 0.009426612841315, 0.0197485925754
                            0.124812312996699, 0.119454688318952, 0.104489989820068, 0.082947830292278,
                            0.058983880135427, 0.036822680065252, 0.019748592575455, 0.009426612841315,
                            0.005719569452904};
-// deemp.h f_colorlpi (1-pole IIR; the HQ default uses it for I and Q)
+// deemp.h f_colorlpi (1-pole IIR; the HQ default uses it for I and Q) and f_colorlpq (-Q: Q)
 constexpr double LPI_B0 = 2.267438981796600e-01, LPI_B1 = 2.267438981796600e-01;
 constexpr double LPI_A1 = -5.465122036406802e-01;
+constexpr double LPQ_B0 = 1.169303716013410e-01, LPQ_B1 = 1.169303716013410e-01;
+constexpr double LPQ_A1 = -7.661392567973181e-01;
+// deemp.h f_nrc (17-tap high pass used by DoCNR)
+const double NRC_B[17] = {
+    -3.148569668063267e-03, -4.941974513425438e-03, -9.929538598536455e-03, -1.787793973911701e-02,
+    -2.783702315543740e-02, -3.829928032339736e-02, -4.750186865627083e-02, -5.380281552534787e-02,
+    9.469899799540406e-01,  -5.380281552534787e-02, -4.750186865627083e-02, -3.829928032339737e-02,
+    -2.783702315543740e-02, -1.787793973911701e-02, -9.929538598536455e-03, -4.941974513425442e-03,
+    -3.148569668063267e-03};
+
+// the options main() sets before Process runs (values as typed on the command line)
+struct Opts {
+  double black_ire = 7.5, brightness = 236, nr_y = 1.0, nr_c = 0.0;
+  int bw = 0, adaptive2d = 1, colorlpf = 1, colorlpf_hq = 1, linesout = 480, debugline = -1000;
+};
 
 struct YIQ { double y = 0, i = 0, q = 0; };
 
@@ -75,17 +92,29 @@ double u16_to_ire_of(double v) {
   return -40 + ((double)level - IREBASE) / IRESCALE;
 }
 
-struct Comb {
-  double aburstlev = -1;          // EMA of the burst level, global across frames
-  double nr_x[25] = {0};          // f_hpy input history x[0] newest, across lines and frames
-
-  double nr_feed(double v) {      // Filter::feed with a = {1}: y = sum_o (b[o] / 1.0) * x[o]
-    std::memmove(&nr_x[1], &nr_x[0], sizeof(double) * 24);
-    nr_x[0] = v;
+// Filter::feed of an FIR (a = {1}): y = sum_o (b[o] / 1.0) * x[o], history across calls
+template <int N>
+struct Fir {
+  const double* b;
+  double x[N] = {0};
+  double feed(double v) {
+    std::memmove(&x[1], &x[0], sizeof(double) * (N - 1));
+    x[0] = v;
     double y0 = 0;
-    for (int o = 0; o < 25; o++) y0 += (NR_B[o] / 1.0) * nr_x[o];
+    for (int o = 0; o < N; o++) y0 += (b[o] / 1.0) * x[o];
     return y0;
   }
+};
+
+struct Comb {
+  double aburstlev = -1;          // EMA of the burst level, global across frames
+  Opts o;
+  // f_hpy, f_hpi, f_hpq (the Comb members DoYNR / DoCNR feed; never reset)
+  Fir<25> hpy{NR_B};
+  Fir<17> hpi{NRC_B}, hpq{NRC_B};
+  int firstline() const { return (o.linesout == IN_Y) ? 20 : 38; }
+  double nr_y() const { return o.nr_y * IRESCALE; }   // main(): nr_y *= irescale
+  double nr_c() const { return o.nr_c * IRESCALE; }
 
   // prev / next: the frames before and after `raw` for the 3D path (-d 3 -F),
   // null for 2D; core / range: p_3dcore / p_3drange (already times irescale)
@@ -123,6 +152,7 @@ struct Comb {
           kn /= 2;
           kp = clampd(1 - (kp / P_2DRANGE), 0, 1);
           kn = clampd(1 - (kn / P_2DRANGE), 0, 1);
+          if (!o.adaptive2d) kn = kp = 1.0;
           double sc = 1.0;
           if (kn != 0 || kp != 0) {
             if (kn > (3 * kp)) kp = 0;
@@ -197,10 +227,12 @@ struct Comb {
         cb[l][h].y = line[h];
         cb[l][h].i = si;
         cb[l][h].q = sq;
+        if (o.bw) cb[l][h].i = cb[l][h].q = 0;
       }
     }
-    // ---- AdjustY (lines 38..524): p[h] = p[h + 2] with y += +-I / +-Q
-    for (int l = FIRST_LINE; l < IN_Y; l++) {
+    const int FL = firstline();
+    // ---- AdjustY (lines firstline..524): p[h] = p[h + 2] with y += +-I / +-Q
+    for (int l = FL; l < IN_Y; l++) {
       const bool invertphase = (raw[l * IN_X] == 16384);
       for (int h = 2; h < 842; h++) {
         YIQ y = cb[l][h + 2];
@@ -216,56 +248,79 @@ struct Comb {
         cb[l][h] = y;
       }
     }
-    // ---- FilterIQ (lines 44..524): fresh colorlpi for I and for Q per line, output 2 px back
-    for (int l = 44; l < IN_Y; l++) {
+    // ---- FilterIQ (lines 44..524, f_colorlpf): fresh colorlpi for I and for Q (colorlpq
+    //      without HQ) per line, output 2 px back
+    const double qb0 = o.colorlpf_hq ? LPI_B0 : LPQ_B0, qb1 = o.colorlpf_hq ? LPI_B1 : LPQ_B1;
+    const double qa1 = o.colorlpf_hq ? LPI_A1 : LPQ_A1;
+    for (int l = 44; o.colorlpf && l < IN_Y; l++) {
       double xi[2] = {0, 0}, yi[2] = {0, 0}, xq[2] = {0, 0}, yq[2] = {0, 0};
-      auto feed = [](double* x, double* y, double v) {
+      auto feed = [](double* x, double* y, double v, double b0, double b1, double a1) {
         x[1] = x[0]; y[1] = y[0];
         x[0] = v;
         double y0 = 0;
-        y0 += (LPI_B0 / 1.0) * x[0];
-        y0 += (LPI_B1 / 1.0) * x[1];
-        y0 -= (LPI_A1 / 1.0) * y[1];
+        y0 += (b0 / 1.0) * x[0];
+        y0 += (b1 / 1.0) * x[1];
+        y0 -= (a1 / 1.0) * y[1];
         y[0] = y0;
         return y0;
       };
       double filti = 0, filtq = 0;
       for (int h = 4; h < 840; h++) {
         switch (h % 4) {
-          case 0: case 2: filti = feed(xi, yi, cb[l][h].i); break;
-          case 1: case 3: filtq = feed(xq, yq, cb[l][h].q); break;
+          case 0: case 2: filti = feed(xi, yi, cb[l][h].i, LPI_B0, LPI_B1, LPI_A1); break;
+          case 1: case 3: filtq = feed(xq, yq, cb[l][h].q, qb0, qb1, qa1); break;
         }
         cb[l][h - 2].i = filti;
         cb[l][h - 2].q = filtq;
       }
     }
-    // (VBI copy into rows 0..23 and DoCNR do not reach the written rows)
-    // ---- DoYNR (lines 38..524): persistent FIR fed h = 40..843, output at h + 12
-    for (int l = FIRST_LINE; l < IN_Y; l++) {
+    // ---- VBI copy: rows 0..23 <- raw lines 20..43 (Y, h 4..839; reaches the output with -v)
+    for (int l = 20; l < 44; l++)
+      for (int h = 4; h < 840; h++) cb[l - 20][h].y = raw[l * IN_X + h];
+    // ---- DoYNR (lines firstline..524, nr_y > 0): persistent FIR fed h = 40..843, output at h + 12
+    const double NRY = nr_y();
+    for (int l = FL; NRY > 0 && l < IN_Y; l++) {
       double hp[IN_X + 32] = {0};
-      for (int h = 40; h <= 843; h++) hp[h] = nr_feed(cb[l][h].y);
+      for (int h = 40; h <= 843; h++) hp[h] = hpy.feed(cb[l][h].y);
       for (int h = 40; h < 843; h++) {
         double a = hp[h + 12];
-        if (std::fabs(a) > NR_Y) a = (a > 0) ? NR_Y : -NR_Y;
+        if (std::fabs(a) > NRY) a = (a > 0) ? NRY : -NRY;
         cb[l][h].y -= a;
       }
     }
-    // ---- ToRGB + PostProcess: rows 38..517, x 78..821
-    const double m = BRIGHTNESS * 256 / 100;
-    for (int l = FIRST_LINE; l < IN_Y; l++) {
+    // ---- DoCNR (lines firstline..524, nr_c > 0): persistent FIRs fed h = 60..842, output at h + 12
+    const double NRC = nr_c();
+    for (int l = FL; NRC > 0 && l < IN_Y; l++) {
+      YIQ hp[IN_X + 32];
+      for (int h = 60; h <= 842; h++) {
+        hp[h].i = hpi.feed(cb[l][h].i);
+        hp[h].q = hpq.feed(cb[l][h].q);
+      }
+      for (int h = 60; h < 842; h++) {
+        double ai = hp[h + 12].i, aq = hp[h + 12].q;
+        if (std::fabs(ai) > NRC) ai = (ai > 0) ? NRC : -NRC;
+        if (std::fabs(aq) > NRC) aq = (aq > 0) ? NRC : -NRC;
+        cb[l][h].i -= ai;
+        cb[l][h].q -= aq;
+      }
+    }
+    // ---- ToRGB + PostProcess: rows firstline.., x 78..821; rows past 524 - firstline stay 0 (-v)
+    const double m = o.brightness * 256 / 100;
+    const int out_h = o.linesout;
+    for (int l = FL; l < IN_Y; l++) {
       const double burstlev = raw[l * IN_X + 1] / IRESCALE;
       if (burstlev > 3) {
         if (aburstlev < 0) aburstlev = burstlev;
         aburstlev = (aburstlev * .99) + (burstlev * .01);
       }
-      const int row = l - FIRST_LINE;
-      if (row >= OUT_H) continue;
+      const int row = l - FL;
+      if (row >= out_h) continue;
       for (int h = OUT_X0; h < OUT_X0 + OUT_W; h++) {
         YIQ yiq = cb[l][h];
         yiq.i *= (10 / aburstlev);
         yiq.q *= (10 / aburstlev);
         double y = u16_to_ire_of(yiq.y);
-        y = (y - BLACK_IRE) * (100 / (100 - BLACK_IRE));
+        y = (y - o.black_ire) * (100 / (100 - o.black_ire));
         const double q = +(yiq.i) / IRESCALE;
         const double i = +(yiq.q) / IRESCALE;
         double r = y + (.956 * i) + (.621 * q);
@@ -274,10 +329,11 @@ struct Comb {
         r = clampd(r * m, 0, 65535);
         g = clampd(g * m, 0, 65535);
         b = clampd(b * m, 0, 65535);
-        uint16_t* o = rgb + ((size_t)row * OUT_W + (h - OUT_X0)) * 3;
-        o[0] = (uint16_t)r;
-        o[1] = (uint16_t)g;
-        o[2] = (uint16_t)b;
+        if (l == (o.debugline + 25)) r = g = b = 0;     // -l: the debug line is blacked out
+        uint16_t* op = rgb + ((size_t)row * OUT_W + (h - OUT_X0)) * 3;
+        op[0] = (uint16_t)r;
+        op[1] = (uint16_t)g;
+        op[2] = (uint16_t)b;
       }
     }
   }
@@ -288,11 +344,18 @@ struct Comb {
 extern "C" {
 void* comb2d_create() { return new Comb(); }
 void comb2d_destroy(void* c) { delete static_cast<Comb*>(c); }
-// n frames of 910 x 525 uint16 -> n frames of 744 x 480 x 3 uint16 (rgb48)
+// the comb-ntsc options (doubles: black_ire, brightness, nr_y, nr_c; ints: bw, adaptive2d,
+// colorlpf, colorlpf_hq, linesout, debugline)
+void comb2d_set_opts(void* c, const double* d, const int* i) {
+  Opts& o = static_cast<Comb*>(c)->o;
+  o.black_ire = d[0]; o.brightness = d[1]; o.nr_y = d[2]; o.nr_c = d[3];
+  o.bw = i[0]; o.adaptive2d = i[1]; o.colorlpf = i[2]; o.colorlpf_hq = i[3]; o.linesout = i[4]; o.debugline = i[5];
+}
+// n frames of 910 x 525 uint16 -> n frames of 744 x linesout x 3 uint16 (rgb48)
 void comb2d_process(void* c, int n, const uint16_t* frames, uint16_t* rgb) {
   Comb* cb = static_cast<Comb*>(c);
   for (int f = 0; f < n; f++)
-    cb->process(frames + (size_t)f * IN_X * IN_Y, rgb + (size_t)f * OUT_W * OUT_H * 3);
+    cb->process(frames + (size_t)f * IN_X * IN_Y, rgb + (size_t)f * OUT_W * cb->o.linesout * 3);
 }
 double comb2d_aburstlev(void* c) { return static_cast<Comb*>(c)->aburstlev; }
 
@@ -305,6 +368,7 @@ struct Comb3 {
   int nhist = 0;
 };
 void* comb3d_create() { return new Comb3(); }
+void comb3d_set_opts(void* c, const double* d, const int* i) { comb2d_set_opts(&static_cast<Comb3*>(c)->c, d, i); }
 void comb3d_destroy(void* c) { delete static_cast<Comb3*>(c); }
 int comb3d_process(void* h, int n, const uint16_t* frames, uint16_t* rgb, double core_ire, double range_ire) {
   Comb3* c = static_cast<Comb3*>(h);
@@ -317,7 +381,7 @@ int comb3d_process(void* h, int n, const uint16_t* frames, uint16_t* rgb, double
   const int L = c->nhist + n;
   int out = 0;
   for (int k = 1; k + 1 < L; k++) {
-    c->c.process(&win[(size_t)k * F], rgb + (size_t)out * OUT_W * OUT_H * 3, &win[(size_t)(k - 1) * F],
+    c->c.process(&win[(size_t)k * F], rgb + (size_t)out * OUT_W * c->c.o.linesout * 3, &win[(size_t)(k - 1) * F],
                  &win[(size_t)(k + 1) * F], core, range);
     out++;
   }

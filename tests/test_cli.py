@@ -274,3 +274,78 @@ def test_cli_pal_comb(tmp_path):
     from oracle.comb import CombPAL
     o = CombPAL().process(frames)
     assert np.abs(o.astype(np.int64) - rgb.astype(np.int64)).max() <= 1
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('args,opts,dim', [(['-I', '0', '-N', '1', '-v'], dict(black_ire=0.0, nr_c=1.0, linesout=525), 2),
+                                           (['-d', '3', '-F', '-I', '0', '-b', '200'],
+                                            dict(black_ire=0.0, brightness=200.0), 3),
+                                           (['-B', '-d', '3', '-n', '0', '-Q', '-L'],
+                                            dict(bw=True, nr_y=0.0, colorlpf_hq=False, colorlpf=False), 2)])
+def test_comb_cli_options_match_oracle(args, opts, dim):
+    """comb_ntsc.py with the reference's option letters (the encode scripts' `-I 0`, CNR, -v,
+    -b, -B forcing dim 2, the LPF toggles) against the oracle with the same options."""
+    sys.path.insert(0, HERE)
+    from test_comb import frames_3d
+    from oracle.comb import Comb2D, Comb3D
+    fr = frames_3d(seed=8, n=5)
+    r = subprocess.run([sys.executable, COMB_CLI, '--chunk', '2'] + args, input=fr.tobytes(), capture_output=True,
+                       timeout=600)
+    assert r.returncode == 0, r.stderr[-2000:]
+    exp = Comb2D(**opts).process(fr) if dim == 2 else Comb3D(**opts).process(fr)
+    got = np.frombuffer(r.stdout, dtype=np.uint16).reshape(exp.shape)
+    assert np.abs(got.astype(np.int64) - exp.astype(np.int64)).max() <= 1
+
+
+@pytest.mark.gpu
+def test_comb_cli_8bit_pulldown_and_images(tmp_path):
+    """-8 writes the high bytes (:710-716); -p pairs fields by the line-0 flag word px 13 and
+    the frame code px 14/15 (PostProcess :894-938): a CAV_ODD frame holds its odd rows, the
+    next frame's even rows complete it (written with the held frame code), a CAV_EVEN frame
+    is written whole, a frame without flags writes nothing; -f -o write <base><code>.rgb."""
+    sys.path.insert(0, HERE)
+    from test_comb import frames_3d
+    from oracle.comb import Comb2D
+    fr = frames_3d(seed=9, n=4).copy()
+    fr[:, 0, 13:16] = 0
+    fr[0, 0, 13], fr[0, 0, 15] = 0x8, 11          # CAV_ODD, code 11
+    fr[1, 0, 13], fr[1, 0, 15] = 0x4, 12          # CAV_EVEN, code 12
+    fr[2, 0, 13], fr[2, 0, 15] = 0x0, 13          # no flags: nothing written
+    fr[3, 0, 13], fr[3, 0, 15] = 0x200, 14        # WHITE_EVEN: written whole
+    rgb = Comb2D().process(fr)
+    r = subprocess.run([sys.executable, COMB_CLI, '-8'], input=fr.tobytes(), capture_output=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-2000:]
+    got8 = np.frombuffer(r.stdout, dtype=np.uint8).reshape(rgb.shape)
+    assert np.abs(got8.astype(np.int64) - (rgb >> 8).astype(np.int64)).max() <= 1
+    mix = rgb[0].copy()
+    mix[0::2] = rgb[1][0::2]
+    exp = [(11, mix), (12, rgb[1]), (14, rgb[3])]
+    r = subprocess.run([sys.executable, COMB_CLI, '-p'], input=fr.tobytes(), capture_output=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-2000:]
+    got = np.frombuffer(r.stdout, dtype=np.uint16).reshape(-1, 480, 744, 3)
+    assert got.shape[0] == 3
+    for g, (_, e) in zip(got, exp):
+        assert np.abs(g.astype(np.int64) - e.astype(np.int64)).max() <= 1
+    base = str(tmp_path / 'img')
+    r = subprocess.run([sys.executable, COMB_CLI, '-p', '-f', '-o', base], input=fr.tobytes(), capture_output=True,
+                       timeout=600)
+    assert r.returncode == 0 and r.stdout == b''
+    for code, e in exp:
+        g = np.fromfile(base + '%d.rgb' % code, dtype=np.uint16).reshape(480, 744, 3)
+        assert np.abs(g.astype(np.int64) - e.astype(np.int64)).max() <= 1
+
+
+@pytest.mark.gpu
+def test_cli_comb_args(tmp_path):
+    """lddecode.py --comb --comb-args '-I 0 -N 1 -v': the fused comb with comb-ntsc's options,
+    against the oracle comb with the same options on the written .tbc frames."""
+    cap, gold = _golden_capture(tmp_path)
+    out = tmp_path / 'out'
+    r = run_cli('-l', 3, '--comb', '--comb-args', '-I 0 -N 1 -v', cap, out)
+    assert r.returncode == 0, r.stderr[-2000:]
+    frames = np.fromfile(str(out) + '.tbc', dtype=np.uint16).reshape(-1, 525, 910)
+    rgb = np.fromfile(str(out) + '.rgb', dtype=np.uint16).reshape(-1, 525, 744, 3)
+    assert len(frames) == 3 and len(rgb) == 3
+    from oracle.comb import Comb2D
+    o = Comb2D(black_ire=0.0, nr_c=1.0, linesout=525).process(frames)
+    assert np.abs(o.astype(np.int64) - rgb.astype(np.int64)).max() <= 1

@@ -321,3 +321,115 @@ def test_gpu_comb_burst_chain_bit_exact(warm, monkeypatch):
     assert got.size == ref.size
     assert np.array_equal(got.view(np.int64), ref.view(np.int64)), np.flatnonzero(got != ref)[:10]
     assert st[0] == a
+
+
+# ---- comb-ntsc's options (main's getopt, comb-ntsc.cxx:972-1091) -------------------------
+
+def expected_grey(y_ire, black_ire=7.5, brightness=236.0, nr=True):
+    """RGB::conv of a flat field (no chroma) with -I black_ire / -b brightness."""
+    yu = int(ynr(float(ire_to_u16(y_ire)))) if nr else ire_to_u16(y_ire)
+    y = -40 + (yu - IREBASE) / IRESCALE
+    y = (y - black_ire) * (100 / (100 - black_ire))
+    return float(np.clip(y * brightness * 256 / 100, 0, 65535))
+
+
+@pytest.mark.parametrize('black,bright', [(0.0, 236.0), (7.5, 200.0), (0.0, 120.0)])
+def test_oracle_black_level_and_brightness_kat(black, bright):
+    """-I (encode-ntsc / encode-ralf run `comb -d 3 -I 0`) and -b on a flat grey field."""
+    out = Comb2D(black_ire=black, brightness=bright).process(frame_solid(50.0)[None])[0]
+    core = out[20:460, 40:700].reshape(-1, 3).astype(np.float64)
+    assert np.abs(core - np.floor(expected_grey(50.0, black, bright))).max() <= 1
+
+
+def test_oracle_ynr_off_kat():
+    """-n 0: DoYNR returns before feeding (comb-ntsc.cxx:527-529): the flat field keeps its level."""
+    out = Comb2D(nr_y=0.0).process(frame_solid(50.0)[None])[0]
+    core = out[20:460, 40:700].reshape(-1, 3).astype(np.float64)
+    assert np.abs(core - np.floor(expected_grey(50.0, nr=False))).max() <= 1
+
+
+def test_oracle_bw_has_no_chroma():
+    """-B: SplitIQ zeroes I and Q (:463-465), so a coloured field comes out grey."""
+    out = Comb2D(bw=True).process(frame_solid(40.0, 1500, -900)[None])[0].astype(np.int64)
+    core = out[10:470, 20:720]
+    assert (core[..., 0] == core[..., 1]).all() and (core[..., 1] == core[..., 2]).all()
+
+
+@pytest.mark.parametrize('opts', [dict(colorlpf=False), dict(colorlpf_hq=False), dict(adaptive2d=False)])
+def test_oracle_solid_colour_options_kat(opts):
+    """The colour LPF (either filter) has unit gain at DC and the fixed 2D weights give the
+    adaptive ones' result on a uniform field: a solid colour decodes to the same I = -a, Q = b."""
+    out = Comb2D(**opts).process(frame_solid(40.0, 1500, -900)[None])[0].astype(np.float64)
+    core = out[40:440, 100:700].reshape(-1, 3)
+    assert np.abs(core - np.floor(expected_rgb(40.0, 1500 * -1, -900))).max() <= 1
+
+
+# deemp.h f_nrc (DoCNR's 17-tap high pass): DC gain sum(taps) = 0.5403, not 0
+NRC_SUM = sum([-3.148569668063267e-03, -4.941974513425438e-03, -9.929538598536455e-03, -1.787793973911701e-02,
+               -2.783702315543740e-02, -3.829928032339736e-02, -4.750186865627083e-02, -5.380281552534787e-02,
+               9.469899799540406e-01, -5.380281552534787e-02, -4.750186865627083e-02, -3.829928032339737e-02,
+               -2.783702315543740e-02, -1.787793973911701e-02, -9.929538598536455e-03, -4.941974513425442e-03,
+               -3.148569668063267e-03])
+
+
+@pytest.mark.parametrize('nr_c', [0.5, 2.0, 5.0])
+def test_oracle_cnr_kat(nr_c):
+    """-N: DoCNR (:485-521) subtracts its high pass, clipped to +-nr_c IRE, from I and Q; on
+    a solid colour the high pass is NRC_SUM * I (Q), so I' = I - clip(NRC_SUM * I)."""
+    clip = nr_c * IRESCALE
+    i0, q0 = -1500.0, -900.0
+    i1 = i0 - float(np.clip(NRC_SUM * i0, -clip, clip))
+    q1 = q0 - float(np.clip(NRC_SUM * q0, -clip, clip))
+    out = Comb2D(nr_c=nr_c).process(frame_solid(40.0, 1500, -900)[None])[0].astype(np.float64)
+    core = out[40:440, 100:700].reshape(-1, 3)
+    assert np.abs(core - np.floor(expected_rgb(40.0, i1, q1))).max() <= 1
+
+
+def test_oracle_525_lines_and_debug_line():
+    """-v: 525 rows from line 20 (:486,1013); rows 0..3 show the VBI copy of raw lines 40..43
+    (:876-882), rows 4..15 (lines 24..35, outside SplitIQ) are black, the last 20 rows are
+    never written (0); -l 100 blacks out line 125 (:586-589)."""
+    fr = frame_solid(30.0)
+    fr[40:44, 2:] = ire_to_u16(80.0)
+    out = Comb2D(linesout=525, debugline=100).process(fr[None])[0].astype(np.int64)
+    assert out.shape == (525, 744, 3)
+    assert (out[505:] == 0).all()
+    assert (out[4:16] == 0).all()
+    assert np.abs(out[0:4, 100:700] - np.floor(expected_grey(80.0))).max() <= 1
+    assert (out[125 - 20] == 0).all() and out[124 - 20].min() > 0
+    dflt = Comb2D(debugline=100).process(fr[None])[0]
+    assert (dflt[125 - 38] == 0).all()
+
+
+COMB_OPTION_CASES = [dict(black_ire=0.0), dict(black_ire=0.0, brightness=200.0), dict(nr_y=0.0), dict(nr_y=3.0),
+                     dict(nr_c=2.0), dict(nr_c=0.5, nr_y=0.5), dict(bw=True), dict(linesout=525),
+                     dict(colorlpf=False), dict(colorlpf_hq=False), dict(adaptive2d=False), dict(debug_line=100)]
+
+
+def _opts_for_oracle(o):
+    return {('debugline' if k == 'debug_line' else k): v for k, v in o.items()}
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('opts', COMB_OPTION_CASES)
+def test_gpu_comb_options_match_oracle(gpu_ctx_ntsc, opts):
+    """The GPU comb with comb-ntsc's options (ldg_comb_set_opts) against the oracle: +-1 LSB
+    on noisy colour frames, 2D and 3D (-d 3 -F)."""
+    ctx, _ = gpu_ctx_ntsc
+    fr = frames_3d(seed=17, n=5)
+    ctx.comb_set_opts(**opts)
+    try:
+        ctx.comb_reset()
+        g = ctx.comb_ntsc(fr)
+        o = Comb2D(**_opts_for_oracle(opts)).process(fr)
+        assert g.shape == o.shape
+        d = np.abs(g.astype(np.int64) - o.astype(np.int64))
+        assert d.max() <= 1, d.max()
+        ctx.comb_reset()
+        g3 = ctx.comb_ntsc3d(fr)
+        o3 = Comb3D(**_opts_for_oracle(opts)).process(fr)
+        assert g3.shape == o3.shape
+        assert np.abs(g3.astype(np.int64) - o3.astype(np.int64)).max() <= 1
+    finally:
+        ctx.comb_set_opts()
+        ctx.comb_reset()
