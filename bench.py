@@ -3,12 +3,20 @@
     python bench.py [--gpus N --steps K --warmup W]
     (N > 1: torch.distributed.run, one rank per GPU, weak scaling)
 
-Workload (BASELINE.json configs[1]): 60 s of synthetic NTSC CAV RF, 40 MSPS,
-8-bit, per GPU, synthesised on the GPU straight into HBM (same signal model as
+N = 1 (default; BASELINE.json configs[1]): 60 s of synthetic NTSC CAV RF,
+40 MSPS, 8-bit, synthesised on the GPU straight into HBM (same signal model as
 ldgpu/synth.py).  One step = the full reference decode of that capture:
-RF -> demod -> TBC -> .tbc frames (+ .pcm audio), every frame of the 60 s,
-with the .tbc frames assembled in HBM.  Ranks decode independent captures
-(fields shard by capture; no data-path collective).
+RF -> demod -> TBC -> .tbc frames (+ .pcm audio) -> 2D comb, every frame of the
+60 s, with the frames assembled in HBM.
+
+N > 1 (default under torch.distributed.run; BASELINE.json configs[4], or
+--sharded at any N): ONE 1-hour 40 MSPS NTSC CLV capture field-sharded across
+the ranks (ldgpu/shard.py, as lddecode.py runs it): each rank holds its window
+of the capture in HBM, and one step = the RCCL halo exchange of the window
+tails (batch_isend_irecv between the GPUs' capture buffers), the rank's
+decode, the summary all_gather and chain check, and the exact audio of its
+frames -- strong scaling of a fixed capture.  --independent instead gives
+every rank its own 60 s capture (weak scaling, no data-path collective).
 """
 import argparse
 import contextlib
@@ -48,7 +56,12 @@ def parse():
     ap.add_argument('--gpus', type=int, default=1)
     ap.add_argument('--steps', type=int, default=2)
     ap.add_argument('--warmup', type=int, default=1)
-    ap.add_argument('--seconds', type=float, default=60.0)
+    ap.add_argument('--seconds', type=float, default=None,
+                    help='capture length (default 60 s; 3600 s for the sharded config-5 leg)')
+    ap.add_argument('--sharded', action='store_true',
+                    help='config 5: one 1 h NTSC CLV capture field-sharded across the ranks (default when N > 1)')
+    ap.add_argument('--independent', action='store_true',
+                    help='N > 1: each rank decodes its own capture (weak scaling) instead of the sharded config 5')
     # reads per launch: over the driver's 20 sustained steps 96 beat 128 in 5 of 6 interleaved
     # comparisons (-0.5..-0.9% time, profiles/r02_s92_s93_batch_20step.txt); in 2-step runs
     # 128 had measured +1% (tools/batch_ab2.sh), before the clock settles
@@ -57,6 +70,8 @@ def parse():
     ap.add_argument('--clv', action='store_true',
                     help='CLV timecode instead of CAV picture numbers (captures past 79,999 frames, e.g. 1 h: config C5)')
     ap.add_argument('--cpu-seconds', type=float, default=1.0, help='oracle baseline sample (seconds of RF)')
+    ap.add_argument('--cpu-procs', type=int, default=0,
+                    help='processes of the multi-process CPU baseline (default: the CPUs visible, at most 16)')
     ap.add_argument('--no-cpu', action='store_true')
     ap.add_argument('--no-comb', action='store_true', help='stop at .tbc (skip the 2D comb stage)')
     ap.add_argument('--host-io', action='store_true',
@@ -68,29 +83,202 @@ def parse():
     return ap.parse_args()
 
 
-def cpu_baseline(seconds):
-    """Oracle (numpy restatement of lddecode_core.py) on a bounded sample, one core."""
+def _oracle_decode(data):
+    """One oracle decode (the numpy restatement of lddecode.py / lddecode_core.py), one core;
+    returns (RF samples consumed, frames, seconds)."""
     from threadpoolctl import threadpool_limits
-    from ldgpu.synth import make_capture
     from oracle.capture import FMT_U8
     from oracle.framer import decode_capture
-    data = make_capture(int(40e6 * seconds), 'u8', seed=99)
     # the oracle prints the reference's log lines ('not valid', ...): to stderr, so
     # the JSON line stays the only stdout output
     with threadpool_limits(limits=1), contextlib.redirect_stdout(sys.stderr):
         t0 = time.perf_counter()
-        frames, pcm, meta = decode_capture(data, FMT_U8)
+        frames, pcm, meta = decode_capture(bytes(data), FMT_U8)
         dt = time.perf_counter() - t0
-    consumed = meta[-1]['nextsample'] if meta else 0
-    return {'value': consumed / dt / 1e6, 'unit': 'RF Msamples/s', 'cores': 1, 'kind': 'port',
-            'sample': '%.2f s synthetic NTSC CAV u8 RF -> %d frames through the oracle (numpy restatement of '
-                      'lddecode_core.py), %.1f s wall on 1 core' % (seconds, len(frames), dt),
-            'fields_per_s': 2 * len(frames) / dt}
+    return (meta[-1]['nextsample'] if meta else 0), len(frames), dt
+
+
+def _oracle_worker(args):
+    path, off, n = args
+    with open(path, 'rb') as fh:
+        fh.seek(off)
+        return _oracle_decode(fh.read(n))
+
+
+def cpu_model():
+    try:
+        for line in open('/proc/cpuinfo'):
+            if line.startswith('model name'):
+                return line.split(':', 1)[1].strip()
+    except OSError:
+        pass
+    return 'unknown'
+
+
+def cpu_baseline(capture, seconds, procs):
+    """The oracle on this box's host cores: (i) one process on one core, the
+    reference's own execution model (numpy FFT single-threaded), on the first `seconds` of the
+    benchmark's capture; (ii) `procs` processes at once, one core each, each on its own
+    `seconds` slice of the same capture (field-group sharding of the CPU path).  Bounded
+    samples, not the whole 60 s (about 16 s of CPU per second of RF)."""
+    import multiprocessing as mp
+    import tempfile
+    n = int(40e6 * seconds)
+    consumed, nfr, dt = _oracle_decode(capture[:n])
+    out = {'value': consumed / dt / 1e6, 'unit': 'RF Msamples/s', 'cores': 1, 'kind': 'port',
+           'cpu_model': cpu_model(), 'host_cpus_visible': len(os.sched_getaffinity(0)),
+           'sample': ('the first %.2f s of the benchmark capture (synthetic NTSC u8 RF) -> %d frames through the '
+                      'oracle (numpy restatement of lddecode_core.py), %.1f s wall on 1 core' % (seconds, nfr, dt)),
+           'fields_per_s': 2 * nfr / dt}
+    if procs > 1 and capture.size >= procs * n:
+        with tempfile.NamedTemporaryFile(prefix='ldg_cpu_', suffix='.u8') as fh:
+            fh.write(capture[:procs * n].tobytes())
+            fh.flush()
+            ctx = mp.get_context('spawn')       # no inherited HIP state in the workers
+            t0 = time.perf_counter()
+            with ctx.Pool(procs) as pool:
+                res = pool.map(_oracle_worker, [(fh.name, k * n, n) for k in range(procs)])
+            wall = time.perf_counter() - t0
+        tot = sum(r[0] for r in res)
+        out['multi_process'] = {'value': tot / wall / 1e6, 'unit': 'RF Msamples/s', 'processes': procs,
+                                'cores': procs, 'fields_per_s': 2 * sum(r[1] for r in res) / wall,
+                                'sample': '%d x %.2f s slices of the benchmark capture, one process (one core) each, '
+                                          '%.1f s wall' % (procs, seconds, wall)}
+    return out
 
 
 def progress(rank, what):
     """a heartbeat on stderr (the JSON line stays the only stdout output)"""
     print('[bench rank %d] %s' % (rank, what), file=sys.stderr, flush=True)
+
+
+class CaptureWorkload:
+    """configs[1] (and --independent N > 1): each rank decodes its own capture, 60 s of NTSC
+    (CAV by default) synthesised straight into HBM.  Weak scaling, no data-path collective."""
+
+    def __init__(self, args, dec, rank):
+        self.args, self.dec = args, dec
+        self.nsamp = int(40e6 * (args.seconds or 60.0))
+        t0 = time.perf_counter()
+        # per-rank capture: its own CAV picture-number range and noise seed
+        dec.ctx.synth(self.nsamp, fmt=args.fmt, first_frame=1 + 2000 * (rank % 39), clv=args.clv,
+                      seed=20181015 + rank)
+        dec.use_resident_capture(args.fmt, self.nsamp)
+        self.synth_s = time.perf_counter() - t0
+        self.host_cap = None
+        if args.host_io:
+            if args.fmt != 0:
+                raise SystemExit('--host-io: u8 captures only')
+            self.host_cap = dec.ctx.capture_download(0, self.nsamp)   # as a loader would hold it
+        self.scaling = 'weak'
+        self.data = 'synthetic (GPU-synthesised NTSC %s RF, %s)' % ('CLV' if args.clv else 'CAV', FMT_NAME[args.fmt])
+
+    def step(self):
+        dec, args = self.dec, self.args
+        if self.host_cap is not None:
+            dec.set_capture(self.host_cap, args.fmt)         # H2D of the whole capture inside the step
+            n = dec.decode(sink=lambda fr, au, meta: None, comb=not args.no_comb, comb_sink=lambda rgb: None)
+        else:
+            dec.use_resident_capture(args.fmt, self.nsamp)   # fresh read cache: no reuse across steps
+            n = dec.decode(sink=None, comb=not args.no_comb)
+        return n, dec.last_meta['nextsample']
+
+    def host_capture(self, n):
+        import numpy as np_
+        return self.host_cap[:n] if self.host_cap is not None else \
+            np_.asarray(self.dec.ctx.capture_download(0, min(n, self.nsamp)))
+
+    def config(self, frames):
+        a = self.args
+        return {'workload': '%g s NTSC %s, 40 MSPS %s RF per GPU: RF->demod->TBC->.tbc+.pcm%s'
+                            % (a.seconds or 60.0, 'CLV' if a.clv else 'CAV', FMT_NAME[a.fmt],
+                               '' if a.no_comb else '->2D comb rgb48'),
+                'frames_per_step': frames // max(a.steps, 1), 'batch_reads': a.batch,
+                'parallelism': 'capture-sharded x%d' % int(os.environ.get('WORLD_SIZE', '1')),
+                'io': 'host buffers over PCIe (--host-io)' if a.host_io else 'HBM-resident'}
+
+    def checks(self):
+        nrs = self.dec.frame_numbers       # consecutive picture numbers, all frames present
+        return {'framenr_consecutive': all(b == a + 1 for a, b in zip(nrs, nrs[1:]))}
+
+
+class ShardedWorkload:
+    """configs[4]: ONE 40 MSPS NTSC CLV capture (1 h by default) field-sharded across the
+    ranks exactly as lddecode.py runs it under torch.distributed.run (ldgpu/shard.py):
+    rank k holds its window [lo_k, hi_k) of the capture in HBM -- its own part synthesised
+    on its GPU (as if read from storage), the tail halo [cut_k, hi_k) received from rank k+1.
+    One step: the halo exchange over RCCL (batch_isend_irecv between the GPUs' capture
+    buffers), the rank's decode (frames and the fused 2D comb in HBM, audio inputs archived),
+    the summary all_gather and chain check, and the exact 48 kHz audio of its frames.
+    Strong scaling: the capture is fixed, each rank gets 1/N of it.  The comb's burst-level
+    EMA starts uninitialised on every rank here (lddecode.py's sharded --comb hands the exact
+    state over after the exchange: tests/test_cli.py::test_cli_sharded_two_ranks_equal_single)."""
+
+    def __init__(self, args, dec, rank, world, dist):
+        import torch
+        from ldgpu.shard import shard_bounds, shard_windows
+        self.args, self.dec, self.rank, self.world, self.dist = args, dec, rank, world, dist
+        self.seconds = args.seconds or 3600.0
+        self.total = int(40e6 * self.seconds)
+        spf = dec.rf.samples_per_frame
+        self.windows = shard_windows(shard_bounds(0, self.total, spf, world), spf, self.total)
+        lo, cut, hi = self.windows[rank]
+        t0 = time.perf_counter()
+        dec.ctx.synth(hi - lo, fmt=0, first_frame=1, clv=True, seed=20181015 + rank, start_sample=lo)
+        self.buf = None
+        if world > 1:
+            # the window in a torch CUDA tensor (RCCL sends / receives its tail in place)
+            self.buf = torch.empty(hi - lo, dtype=torch.uint8, device='cuda')
+            dec.ctx.capture_copy_to_device(self.buf.data_ptr(), 0, hi - lo)
+            torch.cuda.synchronize()
+        self.synth_s = time.perf_counter() - t0
+        self.stats = {}
+        self.scaling = 'strong'
+        self.data = 'synthetic (GPU-synthesised NTSC CLV RF, u8; each rank its window of one capture)'
+        self.halo_rccl = False
+
+    def _allgather(self, obj):
+        if self.world == 1:
+            return [obj]
+        out = [None] * self.world
+        self.dist.all_gather_object(out, obj)
+        return out
+
+    def step(self):
+        from ldgpu.shard import decode_sharded, exchange_halo, torch_p2p
+        dec, lo, hi = self.dec, self.windows[self.rank][0], self.windows[self.rank][2]
+        if self.buf is not None:
+            import torch
+            self.halo_rccl = exchange_halo(self.buf, self.rank, self.windows, 0, torch_p2p) or self.halo_rccl
+            torch.cuda.synchronize()
+            dec.set_capture(None, 0, device_ptr=self.buf.data_ptr(), nsamples=hi - lo, first_sample=lo,
+                            total_bytes=self.total)
+        else:
+            dec.use_resident_capture(0, self.total)
+        res = decode_sharded(dec, self.rank, self.world, self._allgather, resident=True,
+                             comb=not self.args.no_comb, stats=self.stats)
+        if not res:
+            return 0, 0
+        first = res[0][3]['fields'][0]['readsample']
+        return len(res), res[-1][3]['nextsample'] - first
+
+    def host_capture(self, n):
+        if self.buf is not None:
+            return self.buf[:n].cpu().numpy()
+        return self.dec.ctx.capture_download(0, n)
+
+    def config(self, frames):
+        a = self.args
+        return {'workload': 'config 5: %g s NTSC CLV, 40 MSPS u8 RF, ONE capture field-sharded across %d GPU(s) '
+                            '(1/%d each, HBM-resident windows, RCCL halo exchange): RF->demod->TBC->.tbc+.pcm%s'
+                            % (self.seconds, self.world, self.world, '' if a.no_comb else '->2D comb rgb48'),
+                'frames_per_step_rank0': frames // max(a.steps, 1), 'batch_reads': a.batch,
+                'parallelism': 'field-group sharded x%d' % self.world, 'io': 'HBM-resident'}
+
+    def checks(self):
+        return {'frames_per_step_all_ranks': self.stats.get('frames_total'),
+                'chain_refixes': self.stats.get('refixes', 0), 'window_misses': self.stats.get('window_misses', 0),
+                'halo_over_rccl': bool(self.halo_rccl)}
 
 
 def main():
@@ -113,29 +301,12 @@ def main():
 
     from ldgpu.decoder import GPUDecoder
     dec = GPUDecoder(system='NTSC', device=local, batch=args.batch)
-    nsamp = int(40e6 * args.seconds)
-    t0 = time.perf_counter()
-    # per-rank capture: its own CAV picture-number range and noise seed
-    dec.ctx.synth(nsamp, fmt=args.fmt, first_frame=1 + 2000 * (rank % 39), clv=args.clv, seed=20181015 + rank)
-    dec.use_resident_capture(args.fmt, nsamp)
-    synth_s = time.perf_counter() - t0
-    progress(rank, 'capture synthesised (%.1f s)' % synth_s)
-
-    host_cap = None
-    if args.host_io:
-        if args.fmt != 0:
-            raise SystemExit('--host-io: u8 captures only')
-        host_cap = dec.ctx.capture_download(0, nsamp)  # the capture in host memory, as a loader would hold it
-
-    def step():
-        if host_cap is not None:
-            dec.set_capture(host_cap, args.fmt)         # H2D of the whole capture inside the step
-            return dec.decode(sink=lambda fr, au, meta: None, comb=not args.no_comb, comb_sink=lambda rgb: None)
-        dec.use_resident_capture(args.fmt, nsamp)      # fresh read cache: no reuse across steps
-        return dec.decode(sink=None, comb=not args.no_comb)
+    sharded = args.sharded or (world > 1 and not args.independent)
+    wl = ShardedWorkload(args, dec, rank, world, dist) if sharded else CaptureWorkload(args, dec, rank)
+    progress(rank, 'capture synthesised (%.1f s)' % wl.synth_s)
 
     for w in range(args.warmup):
-        nfr = step()
+        wl.step()
         progress(rank, 'warm-up step %d done' % (w + 1))
 
     def barrier():
@@ -151,8 +322,9 @@ def main():
     frames = 0
     consumed = 0
     for k in range(args.steps):
-        frames += step()
-        consumed += dec.last_meta['nextsample']
+        nf, ns = wl.step()
+        frames += nf
+        consumed += ns
         progress(rank, 'step %d done' % (k + 1))
     barrier()
     dt = time.perf_counter() - t0
@@ -170,9 +342,7 @@ def main():
     # figure a kernel trace of this command reports for ldg_k_demod_iso (profiles/)
     iso_reads, iso_ms = dec.demod_isolated(ISO_ITERS)
     reads_timed = dec.stats['reads'] - reads0
-    # sanity on the full-size output: consecutive CAV picture numbers, all frames present
-    nrs = dec.frame_numbers
-    consecutive = all(b == a + 1 for a, b in zip(nrs, nrs[1:]))
+    checks = wl.checks()
 
     if dist is not None:
         import torch
@@ -190,7 +360,6 @@ def main():
             dist.destroy_process_group()
         return
 
-    disc = 'CLV' if args.clv else 'CAV'
     msps = consumed_all / dt_max / 1e6
     fields_s = 2 * frames_all / dt_max
     # Roofline of the dominant kernel, the demod (the one kernel that consumes the capture and
@@ -248,29 +417,27 @@ def main():
     }
     if not args.no_comb:
         roofline['bytes_per_sample_with_comb'] = round(bps + NTSC_COMB_BYTES_PER_SAMPLE, 4)
-    cpu = None if args.no_cpu else cpu_baseline(args.cpu_seconds)
+    cpu = None
+    if not args.no_cpu and world == 1 and args.fmt == 0:
+        # the capture in host memory, as a loader would read it (the CPU path's input)
+        cap = wl.host_capture(int(40e6 * args.cpu_seconds) * max(1, args.cpu_procs or 16))
+        procs = args.cpu_procs or min(16, len(os.sched_getaffinity(0)))
+        cpu = cpu_baseline(cap, args.cpu_seconds, procs)
     line = {
         'metric': 'RF Msamples/s (40 MSPS NTSC, full RF->.tbc decode)', 'value': round(msps, 3),
         'unit': 'RF Msamples/s', 'n_gpus': world, 'steps': args.steps, 'warmup': args.warmup,
-        'ms_per_step': round(dt_max / args.steps * 1e3, 3), 'higher_is_better': True, 'scaling': 'weak',
-        'vs_baseline': None, 'dtype': 'f64',
-        'data': 'synthetic (GPU-synthesised NTSC %s RF, %s)' % (disc, FMT_NAME[args.fmt]),
-        'config': {'workload': '%g s NTSC %s, 40 MSPS %s RF per GPU: RF->demod->TBC->.tbc+.pcm%s'
-                               % (args.seconds, disc, FMT_NAME[args.fmt], '' if args.no_comb else '->2D comb rgb48'),
-                   'frames_per_step': frames // max(args.steps, 1), 'batch_reads': args.batch,
-                   'parallelism': 'capture-sharded x%d' % world,
-                   'io': 'host buffers over PCIe (--host-io)' if args.host_io else 'HBM-resident'},
+        'ms_per_step': round(dt_max / args.steps * 1e3, 3), 'higher_is_better': True, 'scaling': wl.scaling,
+        'vs_baseline': None, 'dtype': 'f64', 'data': wl.data, 'config': wl.config(frames),
         'fields_per_s': round(fields_s, 1), 'realtime_x': round(msps / 40.0, 2),
         'roofline': roofline,
         'kernels_ms': {k: round(v[1], 3) for k, v in sorted(stats.items(), key=lambda kv: -kv[1][1])},
         'cpu_baseline': cpu,
-        'checks': {'framenr_consecutive': consecutive, 'synth_s': round(synth_s, 2),
-                   'reads_decoded': dec.stats['reads'], 'reads_used': dec.stats['reads_used'],
-                   'batches': dec.stats['batches'], 'misses': dec.stats.get('misses', 0),
-                   'drain_waits': dec.stats.get('drain_waits', 0),
-                   'host_s': {k: round(dec.stats.get(k, 0.0), 4) for k in ('plan_s', 'gpu_s', 'replay_s', 'flush_s', 'wait_s')},
-                   'miss_sample': dec.stats.get('miss_log', [])[:12],
-                   'inflight_at_wait': dec.stats.get('inflight_at_wait')},
+        'checks': dict(checks, synth_s=round(wl.synth_s, 2), reads_decoded=dec.stats['reads'],
+                       reads_used=dec.stats['reads_used'], batches=dec.stats['batches'],
+                       misses=dec.stats.get('misses', 0), drain_waits=dec.stats.get('drain_waits', 0),
+                       host_s={k: round(dec.stats.get(k, 0.0), 4)
+                               for k in ('plan_s', 'gpu_s', 'replay_s', 'flush_s', 'wait_s')},
+                       inflight_at_wait=dec.stats.get('inflight_at_wait')),
     }
     print(json.dumps(line), flush=True)
     if dist is not None:

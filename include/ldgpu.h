@@ -310,7 +310,8 @@ typedef struct ldg_synth_params {
 } ldg_synth_params;
 int ldg_synth_capture(ldg_ctx* ctx, const ldg_synth_params* p, const double* fir63, const double* emph,
                       const uint32_t* codes, int64_t ncodeframes);
-/* Copy nbytes of the resident capture starting at byte offset to host dst. */
+/* Copy nbytes of the resident capture starting at byte offset to dst (host memory
+ * or a device buffer of the same device). */
 int64_t ldg_capture_download(ldg_ctx* ctx, void* dst, int64_t offset, int64_t nbytes);
 
 /* CX expander for the .pcm stream (cx-expander.cxx:9-117): host code, one

@@ -414,20 +414,30 @@ class Context:
         n = self.lib.ldg_profile_read(self.h, arr, 64)
         return {arr[i].name.decode(): (int(arr[i].launches), float(arr[i].total_ms)) for i in range(min(n, 64))}
 
-    def synth(self, nsamples, fmt=0, first_frame=1, clv=False, seed=20181015, noise=0.02, start_line=100):
-        """Generate a synthetic NTSC capture straight into this context's HBM capture buffer."""
+    def synth(self, nsamples, fmt=0, first_frame=1, clv=False, seed=20181015, noise=0.02, start_line=100,
+              start_sample=0):
+        """Generate a synthetic NTSC capture straight into this context's HBM capture buffer.
+        start_sample: generate samples [start_sample, start_sample + nsamples) of the capture
+        (a shard's window; line timing and frame codes follow the whole capture's)."""
         import scipy.signal as sps
         from .synth import NTSC, FrameCodes, emphasis_filter, FS
         fir = np.ascontiguousarray(sps.firwin(63, 4.4e6 / (FS / 2)), dtype=np.float64)
         b, a = emphasis_filter(NTSC)
         emph = np.array([b[0], b[1], a[1]], dtype=np.float64)
         spl = FS * NTSC['line_us'] / 1e6
+        start_line = start_line + start_sample / spl
         nframes = int((nsamples / spl + start_line) // 525) + 2
         fc = FrameCodes(first_frame, clv, 30)
         codes = np.array([fc.codes(k) for k in range(nframes)], dtype=np.uint32).reshape(-1)
         p = SynthParams(fmt, 0, nsamples, seed, noise, start_line)
         self._check(self.lib.ldg_synth_capture(self.h, C.byref(p), _ptr(fir), _ptr(emph), _ptr(codes, C.c_uint32),
                                                nframes), 'ldg_synth_capture')
+
+    def capture_copy_to_device(self, dst_ptr, offset, nbytes):
+        """Copy resident capture bytes into a device buffer (e.g. a torch CUDA tensor)."""
+        n = self.lib.ldg_capture_download(self.h, C.c_void_p(dst_ptr), offset, nbytes)
+        if n != nbytes:
+            raise LDGError('ldg_capture_download -> %d' % n)
 
     def capture_download(self, offset, nbytes):
         a = np.zeros(nbytes, dtype=np.uint8)

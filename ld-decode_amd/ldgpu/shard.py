@@ -230,11 +230,14 @@ class ShardedDecode:
     """One rank's part of a field-group sharded decode, in two phases."""
 
     def __init__(self, dec, rank, world, start_frame=0, warmup_frames=2, length=None, start_sample=None,
-                 whole_capture=None, spill_dir=None):
+                 whole_capture=None, spill_dir=None, resident=False, comb=False):
         """whole_capture: callable that makes the whole capture resident (the fallback
         when a capture window turns out too small).  spill_dir: where the output
-        frames wait for the exchange (FrameSpill; default: the system temp dir)."""
+        frames wait for the exchange (FrameSpill; default: the system temp dir).
+        resident: the frames stay in HBM (benchmark mode: decode(sink=None), the fused
+        comb with comb=True); nothing is spilled."""
         self.dec, self.rank, self.world = dec, rank, world
+        self.resident, self.comb = resident, comb
         self.whole_capture, self.window_misses = whole_capture, 0
         self.spf = dec.rf.samples_per_frame
         # the whole decode's frame count limit (lddecode.py:49; -l): frames past it are dropped
@@ -258,7 +261,8 @@ class ShardedDecode:
             self.frames.reset()
             try:
                 dec.decode(start_sample=start_sample, stop_sample=stop, keep_from=keep_from, firstframe=firstframe,
-                           archive=True, sink=keep, init_state=init)
+                           archive=True, sink=None if self.resident else keep, init_state=init,
+                           comb=self.comb)
                 return
             except WindowMiss:
                 # a read outside this rank's capture window: decode from the whole capture
@@ -325,23 +329,32 @@ class ShardedDecode:
 
 
 def decode_sharded(dec, rank, world, allgather, sink=None, start_frame=0, length=None, start_sample=None,
-                   whole_capture=None, spill_dir=None):
+                   whole_capture=None, spill_dir=None, resident=False, comb=False, stats=None):
     """Run all phases with `allgather(obj) -> [obj per rank]` (torch.distributed
     all_gather_object, or an in-process stand-in).  Returns this rank's
     [(global_index, frame, pcm, meta)]; the frames are memory-mapped views of the
-    rank's spill file (FrameSpill), valid while the returned list's frames are."""
+    rank's spill file (FrameSpill), valid while the returned list's frames are.
+    resident: frames stay in HBM (benchmark mode) and frame is None."""
     sd = ShardedDecode(dec, rank, world, start_frame, length=length, start_sample=start_sample,
-                       whole_capture=whole_capture, spill_dir=spill_dir)
+                       whole_capture=whole_capture, spill_dir=spill_dir, resident=resident, comb=comb)
     summ = allgather(sd.local())
+    refixes = 0
     for _ in range(world):
         bad = check_chain(summ)
         if not bad:
             break
+        refixes += len(bad)
         mine = sd.refix(summ) if rank in bad else summ[rank]
         summ = allgather(mine)
     if check_chain(summ):
         raise RuntimeError('sharded decode: chain did not converge')
     res = sd.finish(summ)
+    if stats is not None:
+        stats['refixes'] = stats.get('refixes', 0) + refixes
+        stats['window_misses'] = stats.get('window_misses', 0) + sd.window_misses
+        stats['frames_total'] = sum(s['n'] for s in summ)
+    if resident:
+        return [(g, None, a, m) for (g, a, m) in res]
     return [(g, pic, a, m) for (g, a, m), pic in zip(res, sd.frames)]
 
 

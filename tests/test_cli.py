@@ -218,6 +218,35 @@ def test_cli_sharded_two_ranks_equal_single(tmp_path):
     assert json.load(open(tmp_path / 'one.json')) == json.load(open(tmp_path / 'two.json'))
 
 
+@pytest.mark.gpu
+def test_cli_sharded_rccl_halo_equal_single(tmp_path):
+    """With a GPU per rank the capture-window halo travels between the GPUs' capture buffers
+    over RCCL (lddecode.py load_window, ldgpu/shard.py exchange_halo): two ranks on two GPUs
+    write the same .tbc / .pcm / .json as one process.  Needs two visible devices."""
+    import socket
+    import torch
+    if torch.cuda.device_count() < 2:
+        pytest.skip('needs 2 GPUs (the RCCL halo path); a 1-GPU box runs the gloo variant above')
+    from ldgpu.synth import make_capture
+    data = make_capture(int(40e6 * 0.6), 'u8', first_frame=700, seed=14)
+    cap = tmp_path / 'cap.u8'
+    cap.write_bytes(bytes(data))
+    r = run_cli(cap, tmp_path / 'one')
+    assert r.returncode == 0, r.stderr[-2000:]
+    with socket.socket() as sk:
+        sk.bind(('127.0.0.1', 0))
+        port = sk.getsockname()[1]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY='0')
+    r = subprocess.run([sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', '--nproc-per-node', '2',
+                        '--master-addr', '127.0.0.1', '--master-port', str(port), CLI, str(cap),
+                        str(tmp_path / 'two')], capture_output=True, text=True, timeout=600, env=env)
+    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-3000:])
+    assert 'halo from rank 1 over RCCL' in r.stdout
+    for ext in ('.tbc', '.pcm'):
+        assert (tmp_path / ('one' + ext)).read_bytes() == (tmp_path / ('two' + ext)).read_bytes(), ext
+    assert json.load(open(tmp_path / 'one.json')) == json.load(open(tmp_path / 'two.json'))
+
+
 COMB_CLI = os.path.join(ROOT, 'ld-decode_amd', 'comb_ntsc.py')
 
 
