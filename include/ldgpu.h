@@ -268,6 +268,20 @@ int ldg_comb_ntsc3d(ldg_ctx* ctx, int n, const uint16_t* frames, uint16_t* rgb_o
 int ldg_comb_pal(ldg_ctx* ctx, int n, const uint16_t* frames, uint16_t* rgb_out);
 int ldg_sync(ldg_ctx* ctx);
 
+/* The CLI's output path without host round trips: interleave n field pairs into
+ * .tbc frames in HBM (as ldg_assemble_frames), comb them there when rgb_host is
+ * non-NULL (the 2D NTSC comb, ldg_comb_set_opts' options, state as ldg_comb_ntsc),
+ * and copy the frames (and rgb48) to the host buffers asynchronously on the
+ * output stream, overlapped with the next decode.  The buffers must stay valid
+ * (pinned memory from ldg_host_alloc for full copy speed) until ldg_output_wait,
+ * which waits for the last call's copies. */
+int ldg_output_async(ldg_ctx* ctx, int n, const int32_t* top_slots, const int32_t* bottom_slots, uint16_t* tbc_host,
+                     uint16_t* rgb_host);
+int ldg_output_wait(ldg_ctx* ctx);
+/* Page-locked host memory (hipHostMalloc) for ldg_output_async's buffers. */
+int ldg_host_alloc(int64_t nbytes, void** out);
+int ldg_host_free(void* p);
+
 /* ---- in-library kernel timing (HIP events on the context's stream) ------------- */
 typedef struct ldg_kernel_stat {
   char name[48];

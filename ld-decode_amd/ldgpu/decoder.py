@@ -225,6 +225,8 @@ class GPUDecoder:
         self.archive, self.arch_next, self.shard_frames = False, 0, []
         self._out_pending = None           # (frames, pics, audio fields, sink) awaiting their audio
         self.frame_log = None              # callback(lines): the reference's stdout lines of each frame
+        self._obufs = None                 # pinned host rings for the asynchronous output path
+        self._oring = 0
 
     # ---- capture ---------------------------------------------------------------
     def set_capture(self, data, fmt, device_ptr=None, nsamples=None, first_sample=0, total_bytes=None):
@@ -663,6 +665,8 @@ class GPUDecoder:
     def decode(self, start_frame=0, length=None, sink=None, comb=False, comb_sink=None, start_sample=None,
                stop_sample=None, keep_from=None, firstframe=True, archive=False, init_state=None, comb3d=None):
         """Decode frames; sink(frame_u16, pcm_i16, meta) per frame (None: frames stay in HBM).
+        The frame (and comb_sink's rgb48) handed to the sinks is a view of a pinned output
+        buffer that a later batch reuses: copy it to keep it past the call.
 
         comb: also run the 2D NTSC comb (comb-ntsc.cxx dim=2) on every frame, in
         order, as one comb process; comb_sink(rgb48) receives each 480x744x3
@@ -836,6 +840,21 @@ class GPUDecoder:
             pics = None
             if self.comb:
                 self.ctx.comb_ntsc_async(len(frames))     # overlaps the next batch's decode
+        elif not self.comb or (self.sysp.name == 'NTSC' and self.comb3d is None):
+            # frames (and the fused 2D comb) go to pinned host buffers asynchronously on the
+            # output stream (ldg_output_async); the sink sees them at the next flush, after
+            # ldg_output_wait -- no host round trip of the frames through the comb
+            if self._obufs is None:
+                from .native import PinnedBuffer
+                self._obufs = [(PinnedBuffer(), PinnedBuffer()) for _ in range(2)]
+            tb, rb = self._obufs[self._oring]
+            self._oring ^= 1
+            n = len(frames)
+            pics = tb.view(n * H * W).reshape(n, H * W)
+            rgb = rb.view(n * self.ctx.comb_lines * 744 * 3).reshape(n, self.ctx.comb_lines, 744, 3) \
+                if self.comb else None
+            self.ctx.output_async(tops, bots, pics, rgb)
+            pics = (pics, rgb)
         else:
             pics = self.ctx.assemble_frames(tops, bots, W, H)
             if self.comb:
@@ -874,6 +893,12 @@ class GPUDecoder:
         frames, pics, af, sink = self._out_pending
         self._out_pending = None
         pcm, counts, _ = self.ctx.field_audio_collect()
+        if isinstance(pics, tuple):
+            self.ctx.output_wait()                # this batch's frames / rgb48 are on the host now
+            pics, rgb = pics
+            if rgb is not None and self.comb_sink:
+                for r in rgb:
+                    self.comb_sink(r)
         per_frame = [[] for _ in frames]
         for j, (fr_i, x) in enumerate(af):
             if counts[j] < 0:

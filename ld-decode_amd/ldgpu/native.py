@@ -21,7 +21,8 @@ MAX_VSYNCS = 16
 EXPORTS = ['ldg_create', 'ldg_destroy', 'ldg_last_error', 'ldg_set_filters', 'ldg_set_capture',
            'ldg_decode_reads', 'ldg_field_audio', 'ldg_assemble_frames', 'ldg_debug_read',
            'ldg_comb_ntsc', 'ldg_comb_reset', 'ldg_version', 'ldg_device_count', 'ldg_profile_enable',
-           'ldg_profile_read', 'ldg_synth_capture', 'ldg_capture_download', 'ldg_comb_ntsc_async', 'ldg_sync', 'ldg_demod_isolated', 'ldg_comb_set_opts',
+           'ldg_profile_read', 'ldg_synth_capture', 'ldg_capture_download', 'ldg_comb_ntsc_async', 'ldg_sync', 'ldg_demod_isolated', 'ldg_comb_set_opts', 'ldg_output_async', 'ldg_output_wait',
+           'ldg_host_alloc', 'ldg_host_free',
            'ldg_archive_fields', 'ldg_archive_audio', 'ldg_decode_reads_async', 'ldg_decode_reads_wait',
            'ldg_field_audio_async', 'ldg_field_audio_collect', 'ldg_comb_ntsc3d', 'ldg_cx_create', 'ldg_cx_destroy', 'ldg_cx_process', 'ldg_comb_pal', 'ldg_comb_set_state', 'ldg_profile_spans', 'ldg_profile_spans_union']
 
@@ -113,6 +114,10 @@ def load(path=None):
     lib.ldg_comb_ntsc.argtypes = [vp, C.c_int, vp, vp, C.c_int]
     lib.ldg_comb_reset.argtypes = [vp]
     lib.ldg_comb_set_opts.argtypes = [vp, C.POINTER(CombOpts)]
+    lib.ldg_output_async.argtypes = [vp, C.c_int, vp, vp, vp, vp]
+    lib.ldg_output_wait.argtypes = [vp]
+    lib.ldg_host_alloc.argtypes = [C.c_int64, C.POINTER(vp)]
+    lib.ldg_host_free.argtypes = [vp]
     lib.ldg_comb_ntsc_async.argtypes = [vp, C.c_int]
     lib.ldg_comb_ntsc3d.argtypes = [vp, C.c_int, vp, vp, C.POINTER(C.c_int), C.c_double, C.c_double]
     lib.ldg_decode_reads_async.argtypes = [vp, C.c_int, vp, vp, vp]
@@ -146,6 +151,36 @@ def _ptr(a, t=C.c_double):
 
 class LDGError(RuntimeError):
     pass
+
+
+class PinnedBuffer:
+    """Page-locked host memory (ldg_host_alloc) viewed as a numpy uint16 array; grows on demand."""
+
+    def __init__(self):
+        self.lib = load()
+        self.ptr, self.nbytes, self.arr = None, 0, None
+
+    def view(self, count):
+        nbytes = max(2 * count, 2)
+        if nbytes > self.nbytes:
+            self.free()
+            p = C.c_void_p()
+            if self.lib.ldg_host_alloc(nbytes, C.byref(p)) != LDG_OK:
+                raise LDGError('ldg_host_alloc(%d) failed' % nbytes)
+            self.ptr, self.nbytes = p, nbytes
+            self.arr = np.ctypeslib.as_array(C.cast(p, C.POINTER(C.c_uint16)), shape=(nbytes // 2,))
+        return self.arr[:count]
+
+    def free(self):
+        if self.ptr is not None:
+            self.lib.ldg_host_free(self.ptr)
+            self.ptr, self.nbytes, self.arr = None, 0, None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
 
 
 class Context:
@@ -367,6 +402,20 @@ class Context:
         self._check(self.lib.ldg_demod_isolated(self.h, sl.size, sl.ctypes.data, iters, C.byref(ms)),
                     'ldg_demod_isolated')
         return ms.value
+
+    def output_async(self, tops, bottoms, tbc, rgb=None):
+        """ldg_output_async: frames (and the 2D comb's rgb48 when rgb is given) into the host
+        arrays `tbc` / `rgb` (pinned: PinnedBuffer views) on the output stream; returns at once,
+        output_wait() waits for the copies."""
+        n = len(tops)
+        t = np.ascontiguousarray(tops, dtype=np.int32)
+        b = np.ascontiguousarray(bottoms, dtype=np.int32)
+        self._out_keep = (t, b)
+        self._check(self.lib.ldg_output_async(self.h, n, t.ctypes.data, b.ctypes.data, tbc.ctypes.data,
+                                              rgb.ctypes.data if rgb is not None else None), 'ldg_output_async')
+
+    def output_wait(self):
+        self._check(self.lib.ldg_output_wait(self.h), 'ldg_output_wait')
 
     def sync(self):
         self._check(self.lib.ldg_sync(self.h), 'ldg_sync')
