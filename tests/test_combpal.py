@@ -95,3 +95,25 @@ def test_gpu_comb_pal_matches_oracle(gpu_ctx_ntsc):
     assert d.max() <= 1, d.max()
     assert (d > 0).mean() < 1e-3
     ctx.comb_reset()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('wide', [False, True])
+def test_comb_pal_cli_stream(wide):
+    """comb_pal.py as encode-pal's `comb-pal -d 2 -` stream filter: 974-wide rgb48 frames
+    (attic2/comb-pal.cxx:883-884's geometry, what encode-pal's ffmpeg -s 974x576 reads), or
+    the whole 1057 columns with -W; against the oracle on the same frames (+-1 LSB)."""
+    import os
+    import subprocess
+    import sys
+    from oracle.comb import CombPAL
+    cli = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), 'ld-decode_amd', 'comb_pal.py')
+    fr = pal_frames_noisy(seed=6, n=3)
+    r = subprocess.run([sys.executable, cli, '-d', '2', '--chunk', '2'] + (['-W'] if wide else []) + ['-'],
+                       input=fr.tobytes() + b'\x00' * 100, capture_output=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-2000:]
+    exp = CombPAL().process(fr)
+    if not wide:
+        exp = exp[:, :, :974]
+    got = np.frombuffer(r.stdout, dtype=np.uint16).reshape(exp.shape)
+    assert np.abs(got.astype(np.int64) - exp.astype(np.int64)).max() <= 1
