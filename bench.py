@@ -199,7 +199,8 @@ class CaptureWorkload:
 
     def checks(self):
         nrs = self.dec.frame_numbers       # consecutive picture numbers, all frames present
-        return {'framenr_consecutive': all(b == a + 1 for a, b in zip(nrs, nrs[1:]))}
+        ok = all(b == a + 1 for a, b in zip(nrs, nrs[1:]))
+        return {'framenr_consecutive': ok, 'cav_framenr_consecutive': ok}   # (the round-1 key, kept)
 
 
 class ShardedWorkload:

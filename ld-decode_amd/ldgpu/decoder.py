@@ -808,6 +808,8 @@ class GPUDecoder:
             self.stats['replay_s'] += time.perf_counter() - t0
             if self.stats['batches'] % 32 == 0:
                 gc.collect(1)
+            if self.stats['batches'] % 512 == 0:
+                gc.collect(2)                    # the oldest generation too, rarely (long captures)
             tf = time.perf_counter()
             if self.htrace is not None:
                 self.htrace.append((t0, 'replay', len(frames)))
