@@ -309,7 +309,7 @@ def test_cli_pal_comb(tmp_path):
 @pytest.mark.parametrize('args,opts,dim', [(['-I', '0', '-N', '1', '-v'], dict(black_ire=0.0, nr_c=1.0, linesout=525), 2),
                                            (['-d', '3', '-F', '-I', '0', '-b', '200'],
                                             dict(black_ire=0.0, brightness=200.0), 3),
-                                           (['-B', '-d', '3', '-n', '0', '-Q', '-L'],
+                                           (['-d', '3', '-B', '-n', '0', '-Q', '-L'],
                                             dict(bw=True, nr_y=0.0, colorlpf_hq=False, colorlpf=False), 2)])
 def test_comb_cli_options_match_oracle(args, opts, dim):
     """comb_ntsc.py with the reference's option letters (the encode scripts' `-I 0`, CNR, -v,
