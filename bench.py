@@ -98,11 +98,23 @@ def _oracle_decode(data):
     return (meta[-1]['nextsample'] if meta else 0), len(frames), dt
 
 
+SLICE_SHIFT = 170000          # about a quarter field of 40 MSPS NTSC RF
+
+
 def _oracle_worker(args):
+    """One slice of mode (ii).  A slice that starts inside a vertical sync stops the oracle
+    as it stops the reference (vsync within the first 11 peaks, oracle/field.py); such a slice
+    starts a quarter field later instead, as a sharded CPU runner would place its starts."""
+    from oracle.demod import ReferenceCrash
     path, off, n = args
     with open(path, 'rb') as fh:
-        fh.seek(off)
-        return _oracle_decode(fh.read(n))
+        for j in range(4):
+            fh.seek(off + j * SLICE_SHIFT)
+            try:
+                return _oracle_decode(fh.read(n))
+            except ReferenceCrash:
+                if j == 3:
+                    raise
 
 
 def cpu_model():
@@ -130,9 +142,9 @@ def cpu_baseline(capture, seconds, procs):
            'sample': ('the first %.2f s of the benchmark capture (synthetic NTSC u8 RF) -> %d frames through the '
                       'oracle (numpy restatement of lddecode_core.py), %.1f s wall on 1 core' % (seconds, nfr, dt)),
            'fields_per_s': 2 * nfr / dt}
-    if procs > 1 and capture.size >= procs * n:
+    if procs > 1 and capture.size >= procs * n + 3 * SLICE_SHIFT:
         with tempfile.NamedTemporaryFile(prefix='ldg_cpu_', suffix='.u8') as fh:
-            fh.write(capture[:procs * n].tobytes())
+            fh.write(capture[:procs * n + 3 * SLICE_SHIFT].tobytes())
             fh.flush()
             ctx = mp.get_context('spawn')       # no inherited HIP state in the workers
             t0 = time.perf_counter()
@@ -144,6 +156,34 @@ def cpu_baseline(capture, seconds, procs):
                                 'cores': procs, 'fields_per_s': 2 * sum(r[1] for r in res) / wall,
                                 'sample': '%d x %.2f s slices of the benchmark capture, one process (one core) each, '
                                           '%.1f s wall' % (procs, seconds, wall)}
+    return out
+
+
+LDS_PEAK_TBS = 150.0          # ds_read_b64/b128 with every CU streaming (MI355X_MICROARCH.md, LDS)
+
+
+def bound_analysis(sq, traffic, iso_ms):
+    """Which resource the demod sits against, from the committed PMC passes over the same
+    isolated leg (profiles/pmc_traffic.json, tools/pmc_summary.py) and this run's launch time:
+    HBM (PMC bytes / time), LDS (ds bytes / time against ~150 TB/s, and LDS-array busy
+    cycles), VALU issue (wave64 VALU instructions x 4 cycles over the SIMDs' cycles) and
+    the share of wave time parked at s_waitcnt / barriers."""
+    if not sq:
+        return None
+    c, d = sq['per_launch'], sq['derived']
+    out = {'valu_issue_frac': d.get('valu_issue_frac'), 'fp64_share_of_valu_insts': d.get('fp64_share_of_valu_insts'),
+           'lds_array_busy_frac': d.get('lds_array_busy_frac'),
+           'wave_time': {'issuing': d.get('active_inst_any_per_wave_cycle'),
+                         'parked_waitcnt_barrier': d.get('wait_any_per_wave_cycle'),
+                         'issue_stalled': d.get('wait_inst_any_per_wave_cycle')}}
+    if traffic:
+        out['hbm_tbs'] = traffic / (iso_ms * 1e-3) / 1e12
+        out['hbm_frac'] = out['hbm_tbs'] / (HBM_PEAK_GBS / 1e3)
+    if d.get('lds_bytes'):
+        out['lds_bytes_per_launch'] = d['lds_bytes']
+        out['lds_tbs'] = d['lds_bytes'] / (iso_ms * 1e-3) / 1e12
+        out['lds_frac'] = out['lds_tbs'] / LDS_PEAK_TBS
+    out['source'] = 'profiles/pmc_traffic.json demod_iso_sq (rocprofv3 --pmc passes over this bench\'s isolated leg)'
     return out
 
 
@@ -380,7 +420,7 @@ def main():
         try:
             pj = json.load(open(pmc))
             traffic = pj['kernels'].get('demod_iso')
-            lds = pj.get('demod_iso_sq')
+            lds = bound_analysis(pj.get('demod_iso_sq'), traffic, iso_ms)
         except Exception:
             traffic = None
     # the pipeline's own demod launches (co-running with the field kernels, two demod streams
@@ -407,7 +447,7 @@ def main():
         'algorithmic_bytes_per_launch': round(bps * units_iso),
         'traffic_unit': 'bytes per launch, 2*FETCH_SIZE + WRITE_SIZE (profiles/pmc_traffic.json, demod_iso)',
         'traffic_x_algorithmic': (traffic / (bps * units_iso)) if traffic else None,
-        'lds': lds, 'fp64': fp64,
+        'issue': lds, 'fp64': fp64,
         'pipeline': {'launches': dom_launches, 'span_ms': round(span_ms, 4), 'hip_event_ms': round(event_ms, 4),
                      'busy_ms_per_launch': round(busy_ms, 4), 'units_per_launch': round(units_pipe),
                      'achieved_busy': round(bps * units_pipe / (busy_ms * 1e-3) / 1e9, 4),

@@ -1,7 +1,7 @@
 """Summarise tools/profile.sh runs into profiles/: kernel stats, HBM traffic and the
 demod's issue / LDS / FP64 counters per launch.
 
-    python tools/pmc_summary.py gpurun_out/prof/<tag> profiles/<round>_<tag> [gpurun_out/prof/<tag>sq]
+    python tools/pmc_summary.py gpurun_out/prof/<tag> profiles/<round>_<tag> [gpurun_out/prof/<tag>sq ...]
     (then copy <prefix>_pmc_traffic.json to profiles/pmc_traffic.json for bench.py)
 
 Traffic per launch = 2 * FETCH_SIZE + WRITE_SIZE (KiB -> bytes), the gfx950
@@ -16,6 +16,9 @@ reported, and for the isolated demod (ldg_k_demod_iso) the derived figures:
   LDS array busy  LDS_IDX_ACTIVE / BUSY_CU_CYCLES (both per-CU cycle sums)
   bank conflicts  LDS_BANK_CONFLICT / LDS_IDX_ACTIVE (extra cycles per array cycle)
   FP64 executed   64 lanes * (2 FMA_F64 + MUL_F64 + ADD_F64) wave instructions
+  VALU issue      INSTS_VALU * 4 cycles / (1024 SIMDs * GRBM_GUI_ACTIVE / 8 XCDs)
+                  (a wave64 VALU instruction holds its SIMD 4 cycles; FP64 FMA included)
+  LDS bytes       64 * (LDS_LOAD_BANDWIDTH + LDS_STORE_BANDWIDTH)
 """
 import collections
 import csv
@@ -59,17 +62,27 @@ def derived(c):
     if 'SQ_INSTS_VALU_FMA_F64' in c:
         d['fp64_flops_per_launch'] = 64 * (2 * c['SQ_INSTS_VALU_FMA_F64'] + c.get('SQ_INSTS_VALU_MUL_F64', 0) +
                                            c.get('SQ_INSTS_VALU_ADD_F64', 0))
+    if 'SQ_INSTS_VALU' in c and c.get('GRBM_GUI_ACTIVE'):
+        d['valu_issue_frac'] = c['SQ_INSTS_VALU'] * 4 / (1024 * c['GRBM_GUI_ACTIVE'] / 8)
+        d['gpu_cycles_per_xcd'] = c['GRBM_GUI_ACTIVE'] / 8
+    if 'SQ_INSTS_VALU_FMA_F64' in c and 'SQ_INSTS_VALU' in c:
+        d['fp64_share_of_valu_insts'] = (c['SQ_INSTS_VALU_FMA_F64'] + c.get('SQ_INSTS_VALU_MUL_F64', 0) +
+                                         c.get('SQ_INSTS_VALU_ADD_F64', 0)) / c['SQ_INSTS_VALU']
+    if 'SQ_INSTS_LDS_LOAD_BANDWIDTH' in c:
+        d['lds_load_bytes'] = 64 * c['SQ_INSTS_LDS_LOAD_BANDWIDTH']
+        d['lds_store_bytes'] = 64 * c.get('SQ_INSTS_LDS_STORE_BANDWIDTH', 0)
+        d['lds_bytes'] = d['lds_load_bytes'] + d['lds_store_bytes']
     if 'SQ_INSTS_LDS' in c and 'SQ_INSTS_VALU' in c:
         d['lds_insts_per_valu_inst'] = c['SQ_INSTS_LDS'] / max(c['SQ_INSTS_VALU'], 1)
     return d
 
 
-def main(src, dst_prefix, sq_src=None):
+def main(src, dst_prefix, *sq_srcs):
     stats = os.path.join(src, 'trace', 'run_kernel_stats.csv')
     if os.path.exists(stats):
         shutil.copy(stats, dst_prefix + '_kernel_stats.csv')
     cs = counters(src)
-    if sq_src:
+    for sq_src in sq_srcs:
         for k, v in counters(sq_src).items():
             cs.setdefault(k, {}).update(v)
     out, rows = {}, []
@@ -99,4 +112,4 @@ def main(src, dst_prefix, sq_src=None):
 
 
 if __name__ == '__main__':
-    main(*sys.argv[1:4])
+    main(*sys.argv[1:])
