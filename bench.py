@@ -461,8 +461,8 @@ def main():
     cpu = None
     if not args.no_cpu and world == 1 and args.fmt == 0:
         # the capture in host memory, as a loader would read it (the CPU path's input)
-        cap = wl.host_capture(int(40e6 * args.cpu_seconds) * max(1, args.cpu_procs or 16))
         procs = args.cpu_procs or min(16, len(os.sched_getaffinity(0)))
+        cap = wl.host_capture(int(40e6 * args.cpu_seconds) * max(1, procs) + 3 * SLICE_SHIFT)
         cpu = cpu_baseline(cap, args.cpu_seconds, procs)
     line = {
         'metric': 'RF Msamples/s (40 MSPS NTSC, full RF->.tbc decode)', 'value': round(msps, 3),

@@ -525,6 +525,7 @@ extern "C" __global__ __launch_bounds__(256) void ldg_k_comb_out(const uint16_t*
   const double aburst = abl[(size_t)f * O.chain_lines() + (l - O.firstline)];
   const double m = O.bright_m;
   const bool black = row == O.debug_row;
+  const double kc = 10 / aburst, kb = 100 / (100 - O.black_ire);   // per-pixel factors of ToRGB, hoisted
   for (int x = tid; x < OUT_W; x += 256) {
     const int h = x + OUT_X0;
     double yv = s_y[h];
@@ -552,10 +553,10 @@ extern "C" __global__ __launch_bounds__(256) void ldg_k_comb_out(const uint16_t*
       iv = I_at(h);
       qv = Q_at(h);
     }
-    iv *= (10 / aburst);
-    qv *= (10 / aburst);
+    iv *= kc;
+    qv *= kc;
     double y = u16_to_ire_of(yv);
-    y = (y - O.black_ire) * (100 / (100 - O.black_ire));
+    y = (y - O.black_ire) * kb;
     const double q = +(iv) / IRESCALE;
     const double i = +(qv) / IRESCALE;
     double r = y + (.956 * i) + (.621 * q);

@@ -77,21 +77,48 @@ __device__ inline void d05_fill(const D05Src& src, double* s_vid, double* s_out,
   for (int64_t k = vlo + lane; k < hi + 32; k += 64)
     s_vid[k - vlo] = (k >= 0 && k < src.n_out) ? src.dm[k] : 0.0;
   __syncthreads();
-  for (int64_t n = lo + lane; n < hi; n += 64) {
-    const int b = src.block_of(n);
-    const int64_t off = (int64_t)b * BLOCKSTEP;
-    const int cl = block_copylen(b, src.n_out);
-    const int p = (int)(n - off);
-    double s = 0.0;
-    if (p >= 32 && p + 32 < cl) {
-      const double* w = s_vid + (n - vlo) + 32;
-#pragma unroll 5
-      for (int j = 0; j < F05_TAPS; j++) s = __fma_rn(src.h[j], w[-j], s);
-    } else {
-#pragma unroll 5
-      for (int j = 0; j < F05_TAPS; j++) s = __fma_rn(src.h[j], src.vid(b, off, cl, p + 32 - j), s);
+  // D05_ILP outputs per lane at once (n, n + 64, ...): independent FMA chains, each
+  // in the taps' ascending order as in D05Src (the same doubles)
+  constexpr int D05_ILP = 4;
+  for (int64_t n0 = lo + lane; n0 < hi; n0 += 64 * D05_ILP) {
+    bool fast = true;
+#pragma unroll
+    for (int u = 0; u < D05_ILP; u++) {
+      const int64_t n = n0 + 64 * u;
+      if (n >= hi) break;
+      const int b = src.block_of(n);
+      const int p = (int)(n - (int64_t)b * BLOCKSTEP);
+      fast = fast && p >= 32 && p + 32 < block_copylen(b, src.n_out);
     }
-    s_out[n - lo] = s;
+    if (fast && n0 + 64 * (D05_ILP - 1) < hi) {
+      const double* w = s_vid + (n0 - vlo) + 32;
+      double s[D05_ILP] = {};
+#pragma unroll 5
+      for (int j = 0; j < F05_TAPS; j++) {
+        const double hj = src.h[j];
+#pragma unroll
+        for (int u = 0; u < D05_ILP; u++) s[u] = __fma_rn(hj, w[64 * u - j], s[u]);
+      }
+#pragma unroll
+      for (int u = 0; u < D05_ILP; u++) s_out[n0 + 64 * u - lo] = s[u];
+      continue;
+    }
+    for (int64_t n = n0; n < hi && n < n0 + 64 * D05_ILP; n += 64) {
+      const int b = src.block_of(n);
+      const int64_t off = (int64_t)b * BLOCKSTEP;
+      const int cl = block_copylen(b, src.n_out);
+      const int p = (int)(n - off);
+      double s = 0.0;
+      if (p >= 32 && p + 32 < cl) {
+        const double* w = s_vid + (n - vlo) + 32;
+#pragma unroll 5
+        for (int j = 0; j < F05_TAPS; j++) s = __fma_rn(src.h[j], w[-j], s);
+      } else {
+#pragma unroll 5
+        for (int j = 0; j < F05_TAPS; j++) s = __fma_rn(src.h[j], src.vid(b, off, cl, p + 32 - j), s);
+      }
+      s_out[n - lo] = s;
+    }
   }
   __syncthreads();
 }

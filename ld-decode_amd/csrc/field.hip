@@ -712,7 +712,7 @@ extern "C" __global__ __launch_bounds__(64) void ldg_k_linelocs(
 // test below can touch, [s - 128, s + 576) around the line start s, in LDS;
 // a line whose window leaves the read evaluates the FIR per sample instead.
 namespace {
-constexpr int64_t HS_LO = 128, HS_HI = 576;   // calczc [s-1, s+401]; windows within [s-81, s+522]
+constexpr int64_t HS_LO = 96, HS_HI = 544;    // calczc [s-1, s+401]; windows within [s-81, s+522]
 
 template <class Src>
 __device__ void hsync_line(const Src& d05, int64_t len, const SysConst& C, int i, double v, bool lb, int lane,
