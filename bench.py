@@ -262,15 +262,21 @@ class ShardedWorkload:
         self.seconds = args.seconds or 3600.0
         self.total = int(40e6 * self.seconds)
         spf = dec.rf.samples_per_frame
-        self.windows = shard_windows(shard_bounds(0, self.total, spf, world), spf, self.total)
+        w = shard_windows(shard_bounds(0, self.total, spf, world), spf, self.total)
+        # The synthetic "storage": rank k's stored part ends where rank k+1's begins, so each
+        # sample of the capture is synthesised by exactly one rank and every rank sees the
+        # same bytes (a window synthesised on its own starts its carrier phase and noise
+        # afresh); the rest of the window, [lo_{k+1}, hi_k), comes over the halo exchange.
+        self.windows = [(lo, w[k + 1][0] if k + 1 < world else cut, hi) for k, (lo, cut, hi) in enumerate(w)]
         lo, cut, hi = self.windows[rank]
         t0 = time.perf_counter()
-        dec.ctx.synth(hi - lo, fmt=0, first_frame=1, clv=True, seed=20181015 + rank, start_sample=lo)
+        dec.ctx.synth(cut - lo if world > 1 else hi - lo, fmt=0, first_frame=1, clv=True, seed=20181015,
+                      start_sample=lo)
         self.buf = None
         if world > 1:
             # the window in a torch CUDA tensor (RCCL sends / receives its tail in place)
             self.buf = torch.empty(hi - lo, dtype=torch.uint8, device='cuda')
-            dec.ctx.capture_copy_to_device(self.buf.data_ptr(), 0, hi - lo)
+            dec.ctx.capture_copy_to_device(self.buf.data_ptr(), 0, cut - lo)
             torch.cuda.synchronize()
         self.synth_s = time.perf_counter() - t0
         self.stats = {}
@@ -319,7 +325,8 @@ class ShardedWorkload:
     def checks(self):
         return {'frames_per_step_all_ranks': self.stats.get('frames_total'),
                 'chain_refixes': self.stats.get('refixes', 0), 'window_misses': self.stats.get('window_misses', 0),
-                'halo_over_rccl': bool(self.halo_rccl)}
+                'halo_over_rccl': bool(self.halo_rccl),
+                'phase_s': {k: round(self.stats.get(k, 0.0), 4) for k in ('local_s', 'exchange_s', 'finish_s')}}
 
 
 def main():
@@ -476,6 +483,7 @@ def main():
         'checks': dict(checks, synth_s=round(wl.synth_s, 2), reads_decoded=dec.stats['reads'],
                        reads_used=dec.stats['reads_used'], batches=dec.stats['batches'],
                        misses=dec.stats.get('misses', 0), drain_waits=dec.stats.get('drain_waits', 0),
+                       park_redo=dec.stats.get('migrated', 0),
                        host_s={k: round(dec.stats.get(k, 0.0), 4)
                                for k in ('plan_s', 'gpu_s', 'replay_s', 'flush_s', 'wait_s')},
                        inflight_at_wait=dec.stats.get('inflight_at_wait')),

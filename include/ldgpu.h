@@ -67,9 +67,10 @@ extern "C" {
 #define LDG_FS_EOF 5      /* a block of the read lies beyond the capture window    */
 #define LDG_FS_CRASH 6    /* the reference raises uncaught here (documented)       */
 #define LDG_FS_PENDING 7  /* internal                                               */
-#define LDG_FS_MIGRATED 8 /* the read's demod workgroup moved to another CU mid-block
-                           * (compute-wave save/restore on a shared GPU): its result is
-                           * void, decode the read again                              */
+#define LDG_FS_MIGRATED 8 /* the read's per-CU odd-half park was overwritten between its
+                           * store and its reload (another demod workgroup ran on the CU
+                           * while this one was switched out: compute-wave save/restore
+                           * on a shared GPU): its result is void, decode the read again */
 
 #define LDG_VBI_NONE (-2147483647 - 1) /* Python None in Field.vbi */
 
@@ -195,6 +196,12 @@ int ldg_archive_fields(ldg_ctx* ctx, int n, const int32_t* slots, int64_t first)
 /* ldg_field_audio over archive entries. */
 int ldg_archive_audio(ldg_ctx* ctx, int n, const int64_t* entries, const double* offsets, int16_t* pcm,
                       int64_t pcm_stride, int32_t* counts, double* next_offsets);
+/* The 48 kHz time-offset chain of downscale_audio (lddecode_core.py:432-437,484)
+ * over n fields of line counts linecounts[] from o0: out[0] = o0, out[k + 1] =
+ * np.arange(out[k], frametime_k + gap, gap)[-1] - frametime_k, in numpy's float
+ * arange arithmetic (host code; a shard replays the earlier shards' transitions
+ * with it).  LDG_EINVAL when a range is empty (the reference's IndexError). */
+int ldg_audio_offsets(double o0, int64_t n, const double* linecounts, double line_period, double* out);
 
 /* Interleave field pairs (top slot, bottom slot) into .tbc frames
  * (outlinelen x frame_lines uint16).  out_is_device: `out` is a device pointer. */

@@ -421,15 +421,27 @@ extern "C" __global__ __launch_bounds__(256) void ldg_k_comb_iq(const double* __
   // and c + 1 (I and Q of one row) read the same pairs (cv[6 + 2k], cv[7 + 2k]).
   const double2* cv2 = reinterpret_cast<const double2*>(cv) + 3;
   double x1 = 0.0, y1 = 0.0;
+  // the feeds of chunk kb + 16 are loaded while chunk kb's steps run (the chain is
+  // then bound by its own FP64 latency, not by a load round trip per chunk)
+  double nx[16];
+#pragma unroll
+  for (int j = 0; j < 16; j++) {
+    const double2 v = cv2[j];
+    nx[j] = q ? v.y : v.x;
+  }
 #pragma unroll 1
   for (int kb = 0; kb < IQ_NS; kb += 16) {
     double xs[16];
 #pragma unroll
     for (int j = 0; j < 16; j++) {
       const int k = kb + j;
+      xs[j] = (k >= IQ_NS - 1) ? 0.0 : (((k & 1) != q) ? nx[j] : -nx[j]);
+    }
+#pragma unroll
+    for (int j = 0; j < 16; j++) {
+      const int k = kb + 16 + j;
       const double2 v = cv2[k < IQ_NS - 1 ? k : 0];
-      const double x = q ? v.y : v.x;
-      xs[j] = (k >= IQ_NS - 1) ? 0.0 : (((k & 1) != q) ? x : -x);
+      nx[j] = q ? v.y : v.x;
     }
 #pragma unroll
     for (int j = 0; j < 16; j += 2) {

@@ -178,6 +178,12 @@ __device__ __forceinline__ void st_pair(double* a, double2 z) {
 // The odd-half park's stores (read back by LDS-DMA on the same CU): plain
 // stores ("nt" measured +1.5%, "sc0" even).
 __device__ __forceinline__ void st_park(double2* a, double2 z) { *a = z; }
+// a parked value's signature (bit pattern of both parts; summed over a thread's stores)
+__device__ __forceinline__ uint32_t park_sig(double2 z) {
+  const uint64_t x = (uint64_t)__double_as_longlong(z.x), y = (uint64_t)__double_as_longlong(z.y);
+  const uint64_t v = x ^ ((y << 29) | (y >> 35));
+  return (uint32_t)v ^ (uint32_t)(v >> 32);
+}
 __device__ __forceinline__ void store_pair(double* o, int m, double2 z, int copylen) {
   const int p = 2 * m;
   const int pw0 = 2 * (m & ~63);
@@ -331,6 +337,7 @@ __device__ __forceinline__ void demod_body(LDG_DEMOD_PARAMS) {
   __shared__ double2 s_tw[TW_LDS_N];           // per-lane FFT twiddles (fft8k.hpp)
   __shared__ IIRAux s_aux;
   __shared__ double s_atan[65];
+  __shared__ uint32_t s_park_sig[1024];        // each thread's first park store's signature
   const CBuf X_{s_x};
   const int tid = threadIdx.x;
   if (tid < 65) s_atan[tid] = c_atan64[tid];   // ordered by the first transform's barrier
@@ -435,7 +442,11 @@ __device__ __forceinline__ void demod_body(LDG_DEMOD_PARAMS) {
       const double2 yk = cmul(X.a[c], Fv(sl.p));
       const double2 yk2 = cmul(conj2(X.b[c]), Fv(M + sl.p));
       X_[sl.p] = cadd(yk, yk2);
-      if (!(kProbe & 256)) st_park(park + SW(sl.p), cmulc(csub(yk, yk2), wk));
+      if (!(kProbe & 256)) {
+        const double2 o = cmulc(csub(yk, yk2), wk);
+        st_park(park + SW(sl.p), o);
+        if (c == 0) s_park_sig[tid] = park_sig(o);         // pair 0 is live on every thread
+      }
       if (sl.pp != sl.p) {
         const double2 ykp = cmul(X.b[c], Fv(sl.pp));
         const double2 ykp2 = cmul(conj2(X.a[c]), Fv(M + sl.pp));
@@ -480,12 +491,24 @@ __device__ __forceinline__ void demod_body(LDG_DEMOD_PARAMS) {
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+
   }
-  // The park is private to this CU only while this workgroup stays on it: a
-  // workgroup that compute-wave save/restore resumed on another CU (a shared or
-  // oversubscribed GPU) may have read back a park another workgroup rewrote.
-  // Flag the read: the host decodes it again (FS_MIGRATED).
-  if (tid == 0 && cu_slot() != my_cu) status[slot] = FS_MIGRATED;
+#ifndef LDG_NO_PARK_CHECK   // (timing probes only)
+  if (!(kProbe & (16 | 256))) {
+    // The park is private to this CU only while no other demod workgroup runs on
+    // it between this one's stores and its reload.  Compute-wave save/restore (a
+    // shared or oversubscribed GPU) can break that -- this workgroup switched
+    // out, another one parking on the CU, this one resumed on the same CU or
+    // another.  Each thread re-reads the first value it parked from the park
+    // (after the reload, so an overwrite before it is still there to see) and
+    // compares its signature: a foreign workgroup's wave stores the same slots as
+    // this one's wave, in the same order, so any of its stores that landed
+    // includes that first slot of each of its threads.  A mismatch flags the
+    // read and the host decodes it again (FS_MIGRATED).
+    const double2 pv = park[SW(slot_of(tid, 0).p)];
+    if (park_sig(pv) != s_park_sig[tid]) status[slot] = FS_MIGRATED;
+  }
+#endif
   double* ph = reinterpret_cast<double*>(s_x);    // plain (unswizzled) phase scratch
 #pragma unroll
   for (int q = 0; q < 8; q++) ph[tid + T * q] = tho[q];

@@ -462,8 +462,8 @@ class GPUDecoder:
         import bisect
         for k, sl, inf in zip(keys, slots, infos):
             if inf.status == native.FS_MIGRATED:
-                # the demod workgroup changed CU mid-block (shared GPU): the read is void and
-                # stays undecoded; the replay's miss decodes it again
+                # the demod's park was overwritten under it (compute-wave save/restore on a
+                # shared GPU): the read is void and stays undecoded; the replay's miss decodes it again
                 self.stats['migrated'] = self.stats.get('migrated', 0) + 1
                 continue
             self.cache[k] = (sl, inf)
@@ -874,8 +874,11 @@ class GPUDecoder:
             # audio deferred: archive the fields' audio inputs, record the chain positions
             if af:
                 self.ctx.archive_fields([x.slot for _, x in af], self.arch_next)
+            by_frame = [[] for _ in frames]
+            for j, (fi, x) in enumerate(af):
+                by_frame[fi].append((self.arch_next + j, x.tidx))
             for i, fr in enumerate(frames):
-                ents = [(self.arch_next + j, x.tidx) for j, (fi, x) in enumerate(af) if fi == i]
+                ents = by_frame[i]
                 self.shard_frames.append({'index': fr.index, 'start': int(fr.start), 'tstart': fr.tstart,
                                           'nextsample': int(fr.nextsample),
                                           'audio': ents, 'vbi': dict(fr.vbi), 'fields': fr.fields,

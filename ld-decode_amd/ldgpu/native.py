@@ -24,7 +24,8 @@ EXPORTS = ['ldg_create', 'ldg_destroy', 'ldg_last_error', 'ldg_set_filters', 'ld
            'ldg_profile_read', 'ldg_synth_capture', 'ldg_capture_download', 'ldg_comb_ntsc_async', 'ldg_sync', 'ldg_demod_isolated', 'ldg_comb_set_opts', 'ldg_output_async', 'ldg_output_wait',
            'ldg_host_alloc', 'ldg_host_free',
            'ldg_archive_fields', 'ldg_archive_audio', 'ldg_decode_reads_async', 'ldg_decode_reads_wait',
-           'ldg_field_audio_async', 'ldg_field_audio_collect', 'ldg_comb_ntsc3d', 'ldg_cx_create', 'ldg_cx_destroy', 'ldg_cx_process', 'ldg_comb_pal', 'ldg_comb_set_state', 'ldg_profile_spans', 'ldg_profile_spans_union']
+           'ldg_field_audio_async', 'ldg_field_audio_collect', 'ldg_comb_ntsc3d', 'ldg_cx_create', 'ldg_cx_destroy', 'ldg_cx_process', 'ldg_comb_pal', 'ldg_comb_set_state', 'ldg_profile_spans', 'ldg_profile_spans_union',
+           'ldg_audio_offsets']
 
 
 class FieldInfo(C.Structure):
@@ -139,6 +140,7 @@ def load(path=None):
     lib.ldg_cx_create.argtypes = [C.POINTER(vp)]
     lib.ldg_cx_destroy.argtypes = [vp]
     lib.ldg_cx_process.argtypes = [vp, C.c_int64, vp, vp]
+    lib.ldg_audio_offsets.argtypes = [C.c_double, C.c_int64, vp, C.c_double, vp]
     lib.ldg_version.restype = C.c_char_p
     lib.ldg_device_count.restype = C.c_int
     _lib = lib
@@ -261,7 +263,7 @@ class Context:
                     'ldg_decode_reads')
         out = list(info)
         for _ in range(3):
-            # a read whose demod workgroup moved CU mid-block (FS_MIGRATED) is void: decode it again
+            # a read whose odd-half park another demod workgroup overwrote (FS_MIGRATED) is void: decode it again
             redo = [i for i, x in enumerate(out) if x.status == FS_MIGRATED]
             if not redo:
                 break
@@ -494,6 +496,17 @@ class Context:
         if n < 0:
             raise LDGError('ldg_capture_download -> %d' % n)
         return a[:n]
+
+
+def audio_offsets(o0, linecounts, line_period):
+    """ldg_audio_offsets: [o0, o1, ..., on] of downscale_audio's 48 kHz offset chain over
+    the fields' line counts (host code in the library, no device needed)."""
+    lc = np.ascontiguousarray(linecounts, dtype=np.float64)
+    out = np.zeros(lc.size + 1, dtype=np.float64)
+    rc = load().ldg_audio_offsets(float(o0), lc.size, lc.ctypes.data, float(line_period), out.ctypes.data)
+    if rc != 0:
+        raise IndexError('downscale_audio: empty tick range (the reference raises here)')
+    return out.tolist()
 
 
 class CXExpander:

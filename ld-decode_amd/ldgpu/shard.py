@@ -39,6 +39,8 @@ the rank re-runs with the whole capture.
 """
 import tempfile
 
+import math
+
 import numpy as np
 
 from .decoder import WindowMiss
@@ -117,11 +119,24 @@ def torch_p2p(ops):
 
 
 def audio_next(offset, linecount, line_period):
-    """downscale_audio's returned next offset (lddecode_core.py:432-437, 484)."""
+    """downscale_audio's returned next offset (lddecode_core.py:432-437, 484):
+    np.arange(offset, frametime + gap, gap)[-1] - frametime, without building the
+    array.  numpy's float arange has ceil((stop - start) / step) elements, element 1
+    = start + step and element i >= 2 = start + i * ((start + step) - start)
+    (DOUBLE_fill); an empty range raises IndexError as ticks[-1] would.  Checked
+    equal to the np.arange form (tests/test_shard.py)."""
     frametime = (line_period * linecount) / 1000000
     gap = 1 / 48000.0
-    ticks = np.arange(offset, frametime + gap, gap, dtype=np.double)
-    return ticks[-1] - frametime
+    n = math.ceil(((frametime + gap) - offset) / gap)
+    if n <= 0:
+        raise IndexError('index -1 is out of bounds for axis 0 with size 0')
+    if n == 1:
+        last = offset
+    elif n == 2:
+        last = offset + gap
+    else:
+        last = offset + (n - 1) * ((offset + gap) - offset)
+    return last - frametime
 
 
 def shard_bounds(start, end, spf, world):
@@ -131,11 +146,10 @@ def shard_bounds(start, end, spf, world):
 
 
 def replay_offsets(o0, transitions, line_period):
-    """Offsets after each transition, starting from o0: [o0, o1, ..., on]."""
-    out = [o0]
-    for lc in transitions:
-        out.append(audio_next(out[-1], lc, line_period))
-    return out
+    """Offsets after each transition, starting from o0: [o0, o1, ..., on] (audio_next's
+    recurrence, run in the library: a shard replays every earlier shard's fields)."""
+    from .native import audio_offsets
+    return audio_offsets(o0, transitions, line_period)
 
 
 def check_chain(summaries):
@@ -335,9 +349,13 @@ def decode_sharded(dec, rank, world, allgather, sink=None, start_frame=0, length
     [(global_index, frame, pcm, meta)]; the frames are memory-mapped views of the
     rank's spill file (FrameSpill), valid while the returned list's frames are.
     resident: frames stay in HBM (benchmark mode) and frame is None."""
+    import time
+    t0 = time.perf_counter()
     sd = ShardedDecode(dec, rank, world, start_frame, length=length, start_sample=start_sample,
                        whole_capture=whole_capture, spill_dir=spill_dir, resident=resident, comb=comb)
-    summ = allgather(sd.local())
+    loc = sd.local()
+    t1 = time.perf_counter()
+    summ = allgather(loc)
     refixes = 0
     for _ in range(world):
         bad = check_chain(summ)
@@ -348,8 +366,11 @@ def decode_sharded(dec, rank, world, allgather, sink=None, start_frame=0, length
         summ = allgather(mine)
     if check_chain(summ):
         raise RuntimeError('sharded decode: chain did not converge')
+    t2 = time.perf_counter()
     res = sd.finish(summ)
     if stats is not None:
+        for k, v in (('local_s', t1 - t0), ('exchange_s', t2 - t1), ('finish_s', time.perf_counter() - t2)):
+            stats[k] = stats.get(k, 0.0) + v
         stats['refixes'] = stats.get('refixes', 0) + refixes
         stats['window_misses'] = stats.get('window_misses', 0) + sd.window_misses
         stats['frames_total'] = sum(s['n'] for s in summ)

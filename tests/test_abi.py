@@ -70,3 +70,17 @@ def test_no_cpu_fallback():
         pytest.skip('GPU present')
     with pytest.raises(native.LDGError):
         native.Context('NTSC', 0, max_reads=1)
+
+
+def test_status_and_flag_constants_match_header():
+    """The host's mirrors of the LDG_FS_* status codes and log flags equal the header's
+    (FS_MIGRATED: the demod's per-CU park was left by a migrated workgroup; the host
+    decodes that read again)."""
+    hdr = open(os.path.join(ROOT, 'include', 'ldgpu.h')).read()
+    consts = {k: int(v, 0) for k, v in re.findall(r'#define (LDG_FS_[A-Z_]+)\s+([0-9]+)', hdr)}
+    assert native.FS_MIGRATED == consts['LDG_FS_MIGRATED'] == 8
+    assert re.search(r'#define LDG_LOG_NO_VSYNC \(1 << 16\)', hdr) and native.LOG_NO_VSYNC == 1 << 16
+    for name, v in consts.items():
+        short = name[len('LDG_'):]
+        if hasattr(native, short):
+            assert getattr(native, short) == v, name

@@ -105,6 +105,27 @@ def test_audio_next_is_downscale_audio_recurrence():
         o = o2
 
 
+@pytest.mark.parametrize('line_period', [LINE_PERIOD, 64.0])
+def test_audio_next_closed_form_equals_np_arange(line_period):
+    """audio_next's closed form == np.arange(...)[-1] - frametime bit for bit, over the
+    chain's own offsets and over arbitrary ones (short and empty ranges included)."""
+    rng = np.random.default_rng(7)
+    o = 0.0
+    for i in range(20000):
+        lc = int(rng.choice([262, 263, 312, 313])) if i % 3 else int(rng.integers(1, 700))
+        off = o if i % 2 else float(rng.uniform(-2e-3, 2e-3))
+        frametime = line_period * lc / 1e6
+        ticks = np.arange(off, frametime + 1 / 48000.0, 1 / 48000.0)
+        if ticks.size == 0:
+            with pytest.raises(IndexError):
+                audio_next(off, lc, line_period)
+            continue
+        got = audio_next(off, lc, line_period)
+        assert got == ticks[-1] - frametime
+        assert replay_offsets(off, [lc], line_period)[1] == got      # the library's chain (C)
+        o = got
+
+
 def _worker(rank, world, port, q):
     os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
     dist.init_process_group('gloo', rank=rank, world_size=world)
