@@ -257,12 +257,12 @@ class ShardedWorkload:
 
     def __init__(self, args, dec, rank, world, dist):
         import torch
-        from ldgpu.shard import shard_bounds, shard_windows
+        from ldgpu.shard import decode_bounds, shard_windows
         self.args, self.dec, self.rank, self.world, self.dist = args, dec, rank, world, dist
         self.seconds = args.seconds or 3600.0
         self.total = int(40e6 * self.seconds)
         spf = dec.rf.samples_per_frame
-        w = shard_windows(shard_bounds(0, self.total, spf, world), spf, self.total)
+        w = shard_windows(decode_bounds(self.total, self.total, spf, world)[0], spf, self.total)
         # The synthetic "storage": rank k's stored part ends where rank k+1's begins, so each
         # sample of the capture is synthesised by exactly one rank and every rank sees the
         # same bytes (a window synthesised on its own starts its carrier phase and noise
@@ -273,11 +273,17 @@ class ShardedWorkload:
         dec.ctx.synth(cut - lo if world > 1 else hi - lo, fmt=0, first_frame=1, clv=True, seed=20181015,
                       start_sample=lo)
         self.buf = None
-        if world > 1:
+        # RCCL moves the halo between the GPUs' capture buffers; a rehearsal with more
+        # ranks than GPUs (gloo) moves it through host memory instead
+        self.on_device = dist is not None and dist.get_backend() == 'nccl'
+        if world > 1 and self.on_device:
             # the window in a torch CUDA tensor (RCCL sends / receives its tail in place)
             self.buf = torch.empty(hi - lo, dtype=torch.uint8, device='cuda')
             dec.ctx.capture_copy_to_device(self.buf.data_ptr(), 0, cut - lo)
             torch.cuda.synchronize()
+        elif world > 1:
+            self.buf = torch.zeros(hi - lo, dtype=torch.uint8)
+            self.buf[:cut - lo] = torch.from_numpy(dec.ctx.capture_download(0, cut - lo))
         self.synth_s = time.perf_counter() - t0
         self.stats = {}
         self.scaling = 'strong'
@@ -294,12 +300,15 @@ class ShardedWorkload:
     def step(self):
         from ldgpu.shard import decode_sharded, exchange_halo, torch_p2p
         dec, lo, hi = self.dec, self.windows[self.rank][0], self.windows[self.rank][2]
-        if self.buf is not None:
+        if self.buf is not None and self.on_device:
             import torch
             self.halo_rccl = exchange_halo(self.buf, self.rank, self.windows, 0, torch_p2p) or self.halo_rccl
             torch.cuda.synchronize()
             dec.set_capture(None, 0, device_ptr=self.buf.data_ptr(), nsamples=hi - lo, first_sample=lo,
                             total_bytes=self.total)
+        elif self.buf is not None:
+            exchange_halo(self.buf, self.rank, self.windows, 0, torch_p2p)
+            dec.set_capture(self.buf.numpy(), 0, nsamples=hi - lo, first_sample=lo, total_bytes=self.total)
         else:
             dec.use_resident_capture(0, self.total)
         res = decode_sharded(dec, self.rank, self.world, self._allgather, resident=True,

@@ -160,14 +160,15 @@ def main(argv=None):
     return 0
 
 
-def load_window(dec, raw, fmt, rank, world, start, rccl):
+def load_window(dec, raw, fmt, rank, world, start, rccl, start_frame=0, length=None):
     """This rank's capture window in HBM: its own samples read from storage, the tail
     halo from the next rank (ldgpu/shard.py exchange_halo: RCCL between the capture
     buffers, or gloo through host memory).  Returns what must stay alive."""
     import torch
-    from ldgpu.shard import exchange_halo, sample_byte, shard_bounds, shard_windows, torch_p2p
+    from ldgpu.shard import decode_bounds, exchange_halo, sample_byte, shard_windows, torch_p2p
     nbytes = raw.size
-    bounds = shard_bounds(start, dec.cap_nsamples, dec.rf.samples_per_frame, world)
+    bounds = decode_bounds(dec.cap_nsamples, dec.cap_bytes, dec.rf.samples_per_frame, world, start_frame,
+                           length, start)[0]
     windows = shard_windows(bounds, dec.rf.samples_per_frame, dec.cap_nsamples)
     lo, cut, hi = windows[rank]
     end_b = lambda s: nbytes if s >= dec.cap_nsamples else sample_byte(fmt, s)   # noqa: E731
@@ -205,7 +206,7 @@ def sharded(args, dec, outname, firstframe, num_frames, nextsample, req_frames, 
         dist.all_gather_object(out, obj)
         return out
 
-    keep = load_window(dec, raw, fmt, rank, world, nextsample, rccl)    # noqa: F841 (buffer stays alive)
+    keep = load_window(dec, raw, fmt, rank, world, nextsample, rccl, firstframe, num_frames)   # noqa: F841
 
     def whole():
         print('rank %d: a read left the capture window; using the whole capture' % rank)

@@ -39,11 +39,9 @@ the rank re-runs with the whole capture.
 """
 import tempfile
 
-import math
-
 import numpy as np
 
-from .decoder import WindowMiss
+from .decoder import WindowMiss, arange_last
 from .formats import FMT_LDS, FMT_R30, FMT_S16, FMT_U8
 
 GROUP = 12                      # window cuts on whole packing groups of every format (3 and 4 samples)
@@ -120,29 +118,35 @@ def torch_p2p(ops):
 
 def audio_next(offset, linecount, line_period):
     """downscale_audio's returned next offset (lddecode_core.py:432-437, 484):
-    np.arange(offset, frametime + gap, gap)[-1] - frametime, without building the
-    array.  numpy's float arange has ceil((stop - start) / step) elements, element 1
-    = start + step and element i >= 2 = start + i * ((start + step) - start)
-    (DOUBLE_fill); an empty range raises IndexError as ticks[-1] would.  Checked
-    equal to the np.arange form (tests/test_shard.py)."""
+    np.arange(offset, frametime + gap, gap)[-1] - frametime, without the array
+    (decoder.arange_last); an empty range raises IndexError as ticks[-1] would.
+    ldg_audio_offsets runs the same recurrence in the library (replay_offsets)."""
     frametime = (line_period * linecount) / 1000000
     gap = 1 / 48000.0
-    n = math.ceil(((frametime + gap) - offset) / gap)
-    if n <= 0:
-        raise IndexError('index -1 is out of bounds for axis 0 with size 0')
-    if n == 1:
-        last = offset
-    elif n == 2:
-        last = offset + gap
-    else:
-        last = offset + (n - 1) * ((offset + gap) - offset)
-    return last - frametime
+    try:
+        return arange_last(offset, frametime + gap, gap) - frametime
+    except ValueError:
+        raise IndexError('index -1 is out of bounds for axis 0 with size 0') from None
 
 
 def shard_bounds(start, end, spf, world):
     """Frame-aligned sample boundaries B_0 = start < B_1 < ... < B_world = end."""
     nfr = max(0, (end - start) // spf)
     return [start + (nfr * k // world) * spf for k in range(world)] + [end]
+
+
+def decode_bounds(nsamples, nbytes, spf, world, start_frame=0, length=None, start_sample=None):
+    """The shard boundaries of a decode, its frame limit and its start sample.
+    Frames past the limit (lddecode.py:49, -l; by default the 10-bit EOF guard's
+    count, ~80% of a u8 capture) are dropped, so the shards split only the samples
+    the limit can reach -- the limit's nominal start plus two frames -- instead of
+    the whole capture (whose last fifth a single decode never reads).  Every caller
+    (the decode, the capture windows, the benchmark) uses this one split."""
+    bpf = spf * 5 // 4
+    limit = length if length is not None else nbytes // bpf - start_frame
+    start = start_frame * spf if start_sample is None else start_sample
+    end = min(nsamples, start + (max(limit, 0) + 2) * spf)
+    return shard_bounds(start, end, spf, world), limit, start
 
 
 def replay_offsets(o0, transitions, line_period):
@@ -255,16 +259,16 @@ class ShardedDecode:
         self.whole_capture, self.window_misses = whole_capture, 0
         self.spf = dec.rf.samples_per_frame
         # the whole decode's frame count limit (lddecode.py:49; -l): frames past it are dropped
-        bpf = self.spf * 5 // 4
-        self.limit = length if length is not None else dec.cap_bytes // bpf - start_frame
-        self.start = start_frame * self.spf if start_sample is None else start_sample
-        self.bounds = shard_bounds(self.start, dec.cap_nsamples, self.spf, world)
+        self.bounds, self.limit, self.start = decode_bounds(dec.cap_nsamples, dec.cap_bytes, self.spf, world,
+                                                            start_frame, length, start_sample)
         self.warmup = warmup_frames
         self.frames = FrameSpill(spill_dir)   # this rank's output frames, in order
 
     def _run(self, sink, start_sample, keep_from, firstframe, init=None):
         dec = self.dec
-        stop = self.bounds[self.rank + 1] if self.rank < self.world - 1 else None
+        stop = self.bounds[self.rank + 1]
+        if self.rank == self.world - 1 and stop >= dec.cap_nsamples:
+            stop = None
 
         def keep(pic, audio, meta):
             self.frames.append(pic)

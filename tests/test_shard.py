@@ -14,7 +14,7 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 
 from ldgpu.formats import FMT_LDS, FMT_R30, FMT_U8, bytes_for_samples
-from ldgpu.shard import (audio_next, check_chain, exchange_halo, frame_offsets, halo_plan, replay_offsets,
+from ldgpu.shard import (audio_next, check_chain, decode_bounds, exchange_halo, frame_offsets, halo_plan, replay_offsets,
                          sample_byte, shard_bounds, shard_windows, start_offsets)
 
 LINE_PERIOD = 63.5555555556
@@ -93,6 +93,22 @@ def test_shard_bounds_cover_the_capture():
     b = shard_bounds(0, 2_400_000_000, spf, 8)
     assert b[0] == 0 and b[-1] == 2_400_000_000
     assert all((x % spf) == 0 for x in b[:-1]) and all(x < y for x, y in zip(b, b[1:]))
+
+
+def test_decode_bounds_stop_at_the_frame_limit():
+    """The shards split only the samples the frame limit reaches: a 60 s u8 capture's
+    10-bit EOF guard keeps 1438 of its ~1798 frames, so the last shard ends two frames
+    past frame 1438, not at the end of the capture; -l shortens it further."""
+    spf = 1334667
+    n = 2_400_000_000
+    b, limit, start = decode_bounds(n, n, spf, 4)
+    assert limit == n // (spf * 5 // 4) == 1438 and start == 0
+    assert b[-1] == (limit + 2) * spf < n and b[0] == 0 and all(x < y for x, y in zip(b, b[1:]))
+    b2, limit2, start2 = decode_bounds(n, n, spf, 2, start_frame=10, length=100)
+    assert limit2 == 100 and start2 == 10 * spf and b2[-1] == start2 + 102 * spf
+    # a short capture: the end stays the capture's
+    b3, _, _ = decode_bounds(5 * spf, 5 * spf, spf, 2, length=100)
+    assert b3[-1] == 5 * spf
 
 
 def test_audio_next_is_downscale_audio_recurrence():
@@ -224,7 +240,7 @@ def test_sharded_decode_equals_single_decode(world, windowed):
     raw = np.frombuffer(data, np.uint8)
     n = raw.size
     spf = decs[0].rf.samples_per_frame          # the windows production computes (lddecode.load_window)
-    w = shard_windows(shard_bounds(0, n, spf, world), spf, n)
+    w = shard_windows(decode_bounds(n, n, spf, world)[0], spf, n)
     sds = []
     for r, d in enumerate(decs):
         if windowed:
@@ -240,10 +256,13 @@ def test_sharded_decode_equals_single_decode(world, windowed):
     for sd in sds:
         got += [(pic, a, m) for (g, a, m), pic in zip(sd.finish(summ), sd.frames)]
     assert len(got) == len(want) and all(s['n'] > 0 for s in summ)
-    for (gf, ga, gm), (wf, wa, wm) in zip(got, want):
-        assert gm == wm
-        assert np.array_equal(gf, wf)
-        assert np.array_equal(ga, wa)
+    for i, ((gf, ga, gm), (wf, wa, wm)) in enumerate(zip(got, want)):
+        assert gm == wm, i
+        d = np.flatnonzero(np.asarray(gf) != wf)
+        assert d.size == 0, ('frame %d of %d (ranks %s): %d samples differ, rows %d..%d, max |diff| %d'
+                             % (i, len(got), [s['n'] for s in summ], d.size, d[0] // 910, d[-1] // 910,
+                                np.abs(np.asarray(gf, dtype=np.int64) - wf)[d].max()))
+        assert np.array_equal(ga, wa), i
     if windowed:
         assert all(sd.window_misses == 0 for sd in sds)
 
@@ -264,7 +283,7 @@ def test_sharded_window_miss_falls_back_to_whole_capture():
     ref.decode(sink=lambda fr, au, m: want.append((fr.copy(), au.copy(), m)))
     decs = [GPUDecoder(system='NTSC', batch=8) for _ in range(2)]
     spf = decs[0].rf.samples_per_frame
-    w = shard_windows(shard_bounds(0, n, spf, 2), spf, n, halo_frames=0)
+    w = shard_windows(decode_bounds(n, n, spf, 2)[0], spf, n, halo_frames=0)
     sds = []
     for r, d in enumerate(decs):
         lo, cut, _ = w[r]
