@@ -251,10 +251,15 @@ int ldg_comb_set_opts(ldg_ctx* ctx, const ldg_comb_opts* opts);
  * from the state the previous shard's frames end in (ldgpu/shard.py). */
 int ldg_comb_set_state(ldg_ctx* ctx, double aburstlev);
 /* Asynchronous form for a fused pipeline: comb the first n frames of the
- * context's frame buffer into its rgb buffer on a second stream, overlapped
- * with the next ldg_decode_reads; the next ldg_assemble_frames into the
- * context buffer waits for it.  ldg_sync waits for all outstanding work. */
+ * context's frame buffer (the last ldg_assemble_frames into it) into its rgb
+ * buffer on the comb's own stream, overlapped with the next ldg_decode_reads.
+ * The context alternates two frame buffers, so the next assembly does not wait
+ * for this comb; the one after it (into the same buffer) does.  ldg_sync waits
+ * for all outstanding work.  ldg_comb_async is the same for the context's
+ * system: the NTSC 2D comb, or for PAL the build-defined Y/C decoder of
+ * ldg_comb_pal (576 x 1057 rgb48 per frame). */
 int ldg_comb_ntsc_async(ldg_ctx* ctx, int n);
+int ldg_comb_async(ldg_ctx* ctx, int n);
 /* 3D NTSC comb without optical flow, as `comb-ntsc -d 3 -F -c core -r range`
  * (Process with f = 1 and Split3D(opt_flow = false), comb-ntsc.cxx:369-412,
  * 834-892).  The reference combs frame k once frame k+1 has been read, so a
@@ -273,11 +278,14 @@ int ldg_comb_ntsc3d(ldg_ctx* ctx, int n, const uint16_t* frames, uint16_t* rgb_o
  * states the choices).  n host frames of 1135x625 uint16 in, n rgb48 frames of
  * 1057x576 out; the burst-level EMA carries across calls (ldg_comb_reset). */
 int ldg_comb_pal(ldg_ctx* ctx, int n, const uint16_t* frames, uint16_t* rgb_out);
+/* (ldg_output_async with rgb_host on a PAL context runs this decoder on the
+ * device frames: 576 x 1057 rgb48 per frame.) */
 int ldg_sync(ldg_ctx* ctx);
 
 /* The CLI's output path without host round trips: interleave n field pairs into
  * .tbc frames in HBM (as ldg_assemble_frames), comb them there when rgb_host is
- * non-NULL (the 2D NTSC comb, ldg_comb_set_opts' options, state as ldg_comb_ntsc),
+ * non-NULL (the 2D NTSC comb, ldg_comb_set_opts' options, state as ldg_comb_ntsc;
+ * on a PAL context the Y/C decoder of ldg_comb_pal, 576 x 1057 rgb48 per frame),
  * and copy the frames (and rgb48) to the host buffers asynchronously on the
  * output stream, overlapped with the next decode.  The buffers must stay valid
  * (pinned memory from ldg_host_alloc for full copy speed) until ldg_output_wait,

@@ -683,8 +683,8 @@ class GPUDecoder:
         time offset is known only after the exchange), see self.shard_frames.
         Returns the number of frames decoded."""
         self.comb, self.comb_sink, self.comb3d = comb, comb_sink, (comb3d if comb else None)
-        if (self.comb3d is not None or (comb and self.sysp.name == 'PAL')) and sink is None:
-            raise ValueError('the 3D and PAL combs run on host frames (a sink is required)')
+        if self.comb3d is not None and sink is None:
+            raise ValueError('the 3D comb runs on host frames (a sink is required)')
         self.archive, self.arch_next, self.shard_frames = archive, 0, []
         self.transitions = []
         if comb:
@@ -841,8 +841,8 @@ class GPUDecoder:
             self.ctx.assemble_frames_device(tops, bots)
             pics = None
             if self.comb:
-                self.ctx.comb_ntsc_async(len(frames))     # overlaps the next batch's decode
-        elif not self.comb or (self.sysp.name == 'NTSC' and self.comb3d is None):
+                self.ctx.comb_async(len(frames))          # overlaps the next batch's decode
+        elif not self.comb or self.comb3d is None:
             # frames (and the fused 2D comb) go to pinned host buffers asynchronously on the
             # output stream (ldg_output_async); the sink sees them at the next flush, after
             # ldg_output_wait -- no host round trip of the frames through the comb
@@ -853,8 +853,8 @@ class GPUDecoder:
             self._oring ^= 1
             n = len(frames)
             pics = tb.view(n * H * W).reshape(n, H * W)
-            rgb = rb.view(n * self.ctx.comb_lines * 744 * 3).reshape(n, self.ctx.comb_lines, 744, 3) \
-                if self.comb else None
+            rh, rw = (576, 1057) if self.sysp.name == 'PAL' else (self.ctx.comb_lines, 744)
+            rgb = rb.view(n * rh * rw * 3).reshape(n, rh, rw, 3) if self.comb else None
             self.ctx.output_async(tops, bots, pics, rgb)
             pics = (pics, rgb)
         else:

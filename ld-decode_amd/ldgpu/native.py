@@ -25,7 +25,7 @@ EXPORTS = ['ldg_create', 'ldg_destroy', 'ldg_last_error', 'ldg_set_filters', 'ld
            'ldg_host_alloc', 'ldg_host_free',
            'ldg_archive_fields', 'ldg_archive_audio', 'ldg_decode_reads_async', 'ldg_decode_reads_wait',
            'ldg_field_audio_async', 'ldg_field_audio_collect', 'ldg_comb_ntsc3d', 'ldg_cx_create', 'ldg_cx_destroy', 'ldg_cx_process', 'ldg_comb_pal', 'ldg_comb_set_state', 'ldg_profile_spans', 'ldg_profile_spans_union',
-           'ldg_audio_offsets']
+           'ldg_audio_offsets', 'ldg_comb_async']
 
 
 class FieldInfo(C.Structure):
@@ -120,6 +120,7 @@ def load(path=None):
     lib.ldg_host_alloc.argtypes = [C.c_int64, C.POINTER(vp)]
     lib.ldg_host_free.argtypes = [vp]
     lib.ldg_comb_ntsc_async.argtypes = [vp, C.c_int]
+    lib.ldg_comb_async.argtypes = [vp, C.c_int]
     lib.ldg_comb_ntsc3d.argtypes = [vp, C.c_int, vp, vp, C.POINTER(C.c_int), C.c_double, C.c_double]
     lib.ldg_decode_reads_async.argtypes = [vp, C.c_int, vp, vp, vp]
     lib.ldg_decode_reads_wait.argtypes = [vp, vp]
@@ -396,6 +397,11 @@ class Context:
     def comb_ntsc_async(self, n):
         """ldg_comb_ntsc_async: comb the context's first n device frames on the comb stream."""
         self._check(self.lib.ldg_comb_ntsc_async(self.h, n), 'ldg_comb_ntsc_async')
+
+    def comb_async(self, n):
+        """ldg_comb_async: the context's system's comb (NTSC 2D, or the PAL Y/C decoder) over
+        its first n device frames, on the comb stream."""
+        self._check(self.lib.ldg_comb_async(self.h, n), 'ldg_comb_async')
 
     def demod_isolated(self, slots, iters):
         """Mean HIP-event ms of one demod-only launch (ldg_k_demod_iso) over these live slots."""

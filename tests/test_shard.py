@@ -259,9 +259,19 @@ def test_sharded_decode_equals_single_decode(world, windowed):
     for i, ((gf, ga, gm), (wf, wa, wm)) in enumerate(zip(got, want)):
         assert gm == wm, i
         d = np.flatnonzero(np.asarray(gf) != wf)
-        assert d.size == 0, ('frame %d of %d (ranks %s): %d samples differ, rows %d..%d, max |diff| %d'
-                             % (i, len(got), [s['n'] for s in summ], d.size, d[0] // 910, d[-1] // 910,
-                                np.abs(np.asarray(gf, dtype=np.int64) - wf)[d].max()))
+        if d.size:
+            # which side is off: a second single decode of the same capture
+            again = []
+            ref2 = GPUDecoder(system='NTSC', batch=8)
+            ref2.set_capture(data, 0)
+            ref2.decode(sink=lambda fr, au, m: again.append(fr.copy()))
+            side = ('the first single decode is off' if np.array_equal(again[i], gf) else
+                    'the sharded decode is off' if np.array_equal(again[i], wf) else 'all three differ')
+            assert False, ('frame %d of %d (ranks %s): %d samples differ at %s, max |diff| %d; by a second '
+                           'single decode, %s' % (
+                               i, len(got), [s['n'] for s in summ], d.size,
+                               sorted({(int(x) // 910, int(x) % 910) for x in d})[:6],
+                               np.abs(np.asarray(gf, dtype=np.int64) - wf)[d].max(), side))
         assert np.array_equal(ga, wa), i
     if windowed:
         assert all(sd.window_misses == 0 for sd in sds)

@@ -1,11 +1,12 @@
 """PAL decode throughput (SURVEY §8 d config C3 shape: PAL CLV, 40 MSPS u8), GPU box:
 
-    python tools/pal_bench.py [--seconds 4] [--steps 2]
+    python tools/pal_bench.py [--seconds 4] [--steps 2] [--no-comb]
 
 The capture is synthesised on the host (ldgpu/synth.py, PAL timing, CLV
 timecode) and made resident in HBM before the timed region; each step decodes
-all of it RF -> .tbc + .pcm with the frames left in HBM (no comb: the PAL Y/C
-decoder works on host frames).  Prints one JSON line."""
+all of it RF -> .tbc + .pcm -> the PAL Y/C decoder's rgb48 (ldg_comb_async on
+the assembled frames in HBM; config C3's "comb-pal Y/C path"), frames and rgb
+left in HBM.  Prints one JSON line."""
 import json
 import os
 import sys
@@ -24,19 +25,22 @@ def main():
     data = make_capture(int(40e6 * secs), 'u8', system='PAL', clv=True, first_frame=3000, seed=20181018)
     synth_s = time.perf_counter() - t0
     batch = int(sys.argv[sys.argv.index('--batch') + 1]) if '--batch' in sys.argv else 96
+    comb = '--no-comb' not in sys.argv
     dec = GPUDecoder(system='PAL', batch=batch)
     dec.set_capture(data, 0)
     dec._reset_cache()
-    dec.decode(sink=None)                              # warm-up
+    dec.decode(sink=None, comb=comb)                   # warm-up
     t0 = time.perf_counter()
     frames = consumed = 0
     for _ in range(steps):
         dec._reset_cache()                             # fresh read cache: no reuse across steps
-        frames += dec.decode(sink=None)
+        frames += dec.decode(sink=None, comb=comb)
         consumed += dec.last_meta['nextsample']
+    dec.ctx.sync()
     dt = time.perf_counter() - t0
     msps = consumed / dt / 1e6
-    print(json.dumps({'metric': 'RF Msamples/s (40 MSPS PAL CLV, RF->.tbc+.pcm)', 'value': round(msps, 1),
+    print(json.dumps({'metric': 'RF Msamples/s (40 MSPS PAL CLV, RF->.tbc+.pcm%s)' % ('->PAL Y/C rgb48' if comb else ''),
+                      'value': round(msps, 1),
                       'fields_per_s': round(2 * frames / dt, 1), 'realtime_x': round(msps / 40.0, 1),
                       'frames_per_step': frames // steps, 'seconds_of_rf': secs, 'steps': steps,
                       'synth_s': round(synth_s, 1), 'reads_decoded_total': dec.stats['reads'],
