@@ -168,12 +168,15 @@ constexpr bool kProbeNoStore = false;
 // common case (a wave's 64 pairs all kept or all dropped) branch-free.
 // A channel's 16-byte store, non-temporal ("nt": streamed, the lines still land
 // in L2 for the field kernels; -1.9% demod time against plain stores in an
-// interleaved A/B, "sc1" +13%).  Inline asm: nothing in the kernel reads these
-// addresses back, so the compiler's wait counting need not see them.
+// interleaved A/B, "sc1" +13%).  Through the compiler's builtin, not inline asm:
+// an asm store is opaque to the hazard recognizer, which then does not keep
+// VALU writes off the store's data VGPRs until the store has read them (round 3:
+// under another register allocation whole waves' stores landed corrupted now
+// and then, tools/nondet_probe.py).
 __device__ __forceinline__ void st_pair(double* a, double2 z) {
   typedef double v2d __attribute__((ext_vector_type(2)));
   const v2d zv = {z.x, z.y};
-  asm volatile("global_store_dwordx4 %0, %1, off nt" ::"v"(a), "v"(zv) : "memory");
+  __builtin_nontemporal_store(zv, reinterpret_cast<v2d*>(a));
 }
 // The odd-half park's stores (read back by LDS-DMA on the same CU): plain
 // stores ("nt" measured +1.5%, "sc0" even).
@@ -467,6 +470,24 @@ __device__ __forceinline__ void demod_body(LDG_DEMOD_PARAMS) {
 #pragma clang loop unroll(disable)
   for (int h = 0; h < 2; h++) {
     STAMP(4 + 2 * h);
+#ifndef LDG_NO_PARK_CHECK   // (timing probes only)
+    if (h == 1 && !(kProbe & (16 | 256))) {
+      // The park is private to this CU only while no other demod workgroup runs on
+      // it between this one's stores and its reload.  Compute-wave save/restore (a
+      // shared or oversubscribed GPU) can break that -- this workgroup switched
+      // out, another one parking on the CU, this one resumed on the same CU or
+      // another.  Each thread compares the signature of the first value it parked
+      // with the reloaded LDS image of that slot: a foreign workgroup's wave stores
+      // the same slots as this one's wave, in the same order, so any of its stores
+      // that landed before the reload includes that first slot of each of its
+      // threads (one that lands after the reload does not touch this block's data).
+      // A mismatch flags the read and the host decodes it again (FS_MIGRATED).
+      // (The round-3 form re-read the slot from the park in global memory: one
+      // memory latency per block.)
+      const double2 pv = s_x[SW(slot_of(fresh(tid), 0).p)];
+      if (park_sig(pv) != s_park_sig[tid]) status[slot] = FS_MIGRATED;
+    }
+#endif
     double2 zr[8];
     fft8k_dit<true, true>(s_x, tw, twl, tid, zr);
     if (h == 0) {
@@ -493,22 +514,6 @@ __device__ __forceinline__ void demod_body(LDG_DEMOD_PARAMS) {
     __syncthreads();
 
   }
-#ifndef LDG_NO_PARK_CHECK   // (timing probes only)
-  if (!(kProbe & (16 | 256))) {
-    // The park is private to this CU only while no other demod workgroup runs on
-    // it between this one's stores and its reload.  Compute-wave save/restore (a
-    // shared or oversubscribed GPU) can break that -- this workgroup switched
-    // out, another one parking on the CU, this one resumed on the same CU or
-    // another.  Each thread re-reads the first value it parked from the park
-    // (after the reload, so an overwrite before it is still there to see) and
-    // compares its signature: a foreign workgroup's wave stores the same slots as
-    // this one's wave, in the same order, so any of its stores that landed
-    // includes that first slot of each of its threads.  A mismatch flags the
-    // read and the host decodes it again (FS_MIGRATED).
-    const double2 pv = park[SW(slot_of(tid, 0).p)];
-    if (park_sig(pv) != s_park_sig[tid]) status[slot] = FS_MIGRATED;
-  }
-#endif
   double* ph = reinterpret_cast<double*>(s_x);    // plain (unswizzled) phase scratch
 #pragma unroll
   for (int q = 0; q < 8; q++) ph[tid + T * q] = tho[q];
@@ -563,12 +568,29 @@ __device__ __forceinline__ void demod_body(LDG_DEMOD_PARAMS) {
     pt1 = iir[IIR_P1 + t];
     p151 = iir[IIR_P1 + scan_d15(t & 63)];
     p311 = iir[IIR_P1 + scan_d31(t & 63)];
-    // demod_05 itself is not stored (d05.hpp: consumers rebuild the few samples
-    // they read from the video channel); only its sync detector bits are kept
+    // demod_05 is stored at full rate for refine_linelocs_hsync and the PAL pilot
+    // windows (rebuilding those windows by the 65-tap FIR in the field kernels
+    // instead measured 3.6% slower end to end, profiles/r03_z_d05_ab.txt)
+    double* o = vout + (int64_t)CH_05 * vchan_stride;
 #pragma unroll
     for (int q = 0; q < 8; q++) {
       const int m = t + T * q;
       const double v0 = zr[q].x * inv, v1 = zr[q].y * inv;
+      if (!kProbeNoStore) {
+        // block position p lands at rolled position (p - 32) mod 16384 (even: p0 + 1 never wraps);
+        // the wave's 64 pairs are all kept or all dropped except at the block ends
+        const int p0 = (2 * m - BLOCKCUT_END) & (BLOCKLEN - 1);
+        const int pw0 = (2 * (m & ~63) - BLOCKCUT_END) & (BLOCKLEN - 1);
+        if (pw0 >= BLOCKCUT && pw0 + 127 < BLOCKCUT + copylen) {
+          st_pair(o + p0, make_double2(v0, v1));
+        } else {
+          const bool in0 = p0 >= BLOCKCUT && p0 < BLOCKCUT + copylen;
+          const bool in1 = p0 + 1 >= BLOCKCUT && p0 + 1 < BLOCKCUT + copylen;
+          if (in0 && in1) *reinterpret_cast<double2*>(o + p0) = make_double2(v0, v1);
+          else if (in0) o[p0] = v0;
+          else if (in1) o[p0 + 1] = v1;
+        }
+      }
       // detector bits at UNROLLED block positions 2m, 2m + 1; lanes 8j..8j+7 (pairs
       // of 16 consecutive samples) OR their bits into lane 8j+7 (DPP row shifts)
       const uint32_t f0 = (v0 >= C.sync_lo && v0 <= C.sync_hi) ? 1u : 0u;

@@ -781,31 +781,23 @@ extern "C" __global__ __launch_bounds__(64) void ldg_k_hsync_lines(
   prio_latency();
 
   __shared__ double s_tmp[20];
-  __shared__ double s_vid[HS_LO + HS_HI + 64];
-  __shared__ double s_d05[HS_LO + HS_HI];
   const int lane = threadIdx.x;
   const int slot = smap[blockIdx.x / MAX_LINES];
   const int i = blockIdx.x % MAX_LINES;
   FieldRec* R = recs + slot;
   if (R->status != FS_PENDING) return;
   if (i >= R->nlines) return;
-  const double* dm = video + (int64_t)slot * vread_stride + (int64_t)CH_DEMOD * vchan_stride;
+  // demod_05 as the demod stored it
+  const double* d05 = video + (int64_t)slot * vread_stride + (int64_t)CH_05 * vchan_stride;
   const int64_t len = R->n_out;
-  const D05Src src(dm, d05halo, slot, f05, len, reads[slot].n_blocks);
   const double* L1 = lines + (int64_t)slot * LINES_STRIDE + LL1 * MAX_LINES;
   double* L2 = lines + (int64_t)slot * LINES_STRIDE + LL2 * MAX_LINES;
   int8_t* B = bad + (int64_t)slot * MAX_LINES;
   const double v = L1[i];
   const bool lb = B[i] != 0;
-  const int64_t s0 = py_int(i < 9 ? v - 200 : v);
   double out;
   int flag;
-  if (s0 - HS_LO >= 0 && s0 + HS_HI <= len) {
-    d05_fill(src, s_vid, s_d05, s0 - HS_LO, s0 + HS_HI, lane);
-    hsync_line(D05Win{s_d05, s0 - HS_LO}, len, C, i, v, lb, lane, s_tmp, out, flag);
-  } else {
-    hsync_line(src, len, C, i, v, lb, lane, s_tmp, out, flag);
-  }
+  hsync_line(d05, len, C, i, v, lb, lane, s_tmp, out, flag);
   if (lane == 0) { L2[i] = out; B[i] = (int8_t)flag; }
 }
 

@@ -830,8 +830,8 @@ extern "C" __global__ __launch_bounds__(64) void ldg_k_pilot_lines(const int32_t
   const int pn = (int)(b > a ? b - a : 0);
   const int pm = pn < PW ? pn : PW;
   if (pm > 0) {
-    d05_fill(d5, s_vid, s_d05, b - pm, b, lane);
-    for (int q = lane; q < pm; q += 64) s_pil[q] = dm[b - 1 - q] - s_d05[pm - 1 - q];   // np.flip
+    const double* d05 = video + (int64_t)slot * vread_stride + (int64_t)CH_05 * vchan_stride;
+    for (int q = lane; q < pm; q += 64) s_pil[q] = dm[b - 1 - q] - d05[b - 1 - q];   // np.flip
     __syncthreads();
   }
   if (lane != 0) return;
