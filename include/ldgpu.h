@@ -137,9 +137,9 @@ typedef struct ldg_filters {
    * recurrences; ldg_set_filters checks fpsync = B/A and fvideoburst
    * (fvideopilot) = fvideo * B/A on every bin and fails with LDG_EINVAL otherwise. */
   const double *iir;
-  /* The 65 taps of F05 (firwin(65, 0.5 MHz), lddecode_core.py:199-202): demod_05 is
-   * rebuilt from the demod channel by this FIR where it is read (no full-rate
-   * channel); ldg_set_filters checks fvideo05 = fvideo * DFT(taps) on every bin. */
+  /* Optional: the 65 taps of F05 (firwin(65, 0.5 MHz), lddecode_core.py:199-202).
+   * When given, ldg_set_filters checks fvideo05 = fvideo * DFT(taps) on every bin
+   * (NULL: no check). */
   const double *f05_fir;
 } ldg_filters;
 

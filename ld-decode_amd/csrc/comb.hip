@@ -72,6 +72,19 @@ struct CombOpt {
   __host__ __device__ int chain_lines() const { return IN_Y - firstline; }
 };
 
+// comb-ntsc's defaults as compile-time constants (comb-ntsc.cxx:15-75,1074-1091):
+// the kernels are instantiated for CombOpt (ldg_comb_set_opts) and for this, the
+// options every CLI / benchmark run without comb flags uses; with them folded the
+// kernels keep fewer registers (comb_out 78 VGPRs instead of 95) and no option tests.
+struct CombDefaults {
+  static constexpr int firstline = FIRST_LINE, nrows = OUT_H, out_rows = OUT_H;
+  static constexpr int adaptive2d = 1, bw = 0, colorlpf = 1, lpq = 0, debug_row = -1;
+  static constexpr double black_ire = 7.5, bright_m = 236.0 * 256 / 100, nr_y = 1.0 * IRESCALE, nr_c = 0.0;
+  __host__ __device__ static constexpr int iq_row0() { return 44 - firstline; }
+  __host__ __device__ static constexpr int iq_rows() { return nrows - iq_row0(); }
+  __host__ __device__ static constexpr int chain_lines() { return IN_Y - firstline; }
+};
+
 struct LP3DTaps { double b[17]; };   // lp_3d = fir1(16, 0.1), comb-ntsc.cxx:379
 __constant__ LP3DTaps g_lp3d = {{0.005719569452904, 0.009426612841315, 0.019748592575455, 0.036822680065252,
                                  0.058983880135427, 0.082947830292278, 0.104489989820068, 0.119454688318951,
@@ -282,9 +295,9 @@ extern "C" __global__ __launch_bounds__(256) void ldg_k_comb_burst(const uint16_
 // grid: n * O.nrows workgroups of 256 threads; row r = line r + firstline; cv: [n][nrows][CV_STRIDE].
 // D3: frames[f] has its neighbours at frames[f -+ 1] (core / range: p_3dcore,
 // p_3drange times irescale).
-template <bool D3>
+template <bool D3, class OPT>
 __device__ __forceinline__ void comb_split_row(const uint16_t* __restrict__ frames, double* __restrict__ cvbuf,
-                                               double core, double range, const CombOpt& O) {
+                                               double core, double range, const OPT& O) {
   __shared__ uint16_t s_raw[3][IN_X + 2];                // raw lines l-2, l, l+2
   __shared__ double s_c[3][IN_X];                        // Split1D clp0 of those lines
   __shared__ uint16_t s_pn[D3 ? 2 : 1][IN_X + 2];        // 3D: line l of the previous / next frame
@@ -387,7 +400,11 @@ __device__ __forceinline__ void comb_split_row(const uint16_t* __restrict__ fram
 }
 
 extern "C" __global__ __launch_bounds__(256) void ldg_k_comb_split(const uint16_t* __restrict__ frames,
-                                                                   double* __restrict__ cvbuf, CombOpt O) {
+                                                                   double* __restrict__ cvbuf) {
+  comb_split_row<false>(frames, cvbuf, 0.0, 1.0, CombDefaults{});
+}
+extern "C" __global__ __launch_bounds__(256) void ldg_k_comb_split_opt(const uint16_t* __restrict__ frames,
+                                                                       double* __restrict__ cvbuf, CombOpt O) {
   comb_split_row<false>(frames, cvbuf, 0.0, 1.0, O);
 }
 
@@ -403,8 +420,9 @@ extern "C" __global__ __launch_bounds__(256) void ldg_k_comb_split3(const uint16
 // y = ((0 + b0 x_h) + b1 x_{h-2}) - a1 y_prev in the reference's order
 // (Filter::feed, ld-decoder.h:180-186); Q through f_colorlpq with -Q.
 // grid: ceil(n * iq_rows * 2 / 256) x 256.  iq: [n][iq_rows][2][IQ_NS] outputs.
-extern "C" __global__ __launch_bounds__(256) void ldg_k_comb_iq(const double* __restrict__ cvbuf, int n,
-                                                                double* __restrict__ iq, CombOpt O) {
+template <class OPT>
+__device__ __forceinline__ void comb_iq_lane(const double* __restrict__ cvbuf, int n, double* __restrict__ iq,
+                                             const OPT& O) {
   prio_latency();
 
   const int rows = O.iq_rows();
@@ -462,17 +480,25 @@ extern "C" __global__ __launch_bounds__(256) void ldg_k_comb_iq(const double* __
   }
 }
 
+extern "C" __global__ __launch_bounds__(256) void ldg_k_comb_iq(const double* __restrict__ cvbuf, int n,
+                                                                double* __restrict__ iq) {
+  comb_iq_lane(cvbuf, n, iq, CombDefaults{});
+}
+extern "C" __global__ __launch_bounds__(256) void ldg_k_comb_iq_opt(const double* __restrict__ cvbuf, int n,
+                                                                    double* __restrict__ iq, CombOpt O) {
+  comb_iq_lane(cvbuf, n, iq, O);
+}
+
 // ---- ldg_k_comb_out: AdjustY, the FilterIQ outputs, the VBI copy, DoYNR,
 // DoCNR and ToRGB of one output row.  grid: n * O.out_rows workgroups of 256
 // threads (rows >= O.nrows are the -v frame's never-written bottom rows: 0).
 // For output pixels x >= 78 every FIR tap of DoYNR (h - 12 >= 66 >= 40) and
 // DoCNR (h + 12 - 16 >= 74 >= 60) falls inside the row, so their cross-line
 // histories never reach an output pixel.
-extern "C" __global__ __launch_bounds__(256) void ldg_k_comb_out(const uint16_t* __restrict__ frames,
-                                                                 const double* __restrict__ cvbuf,
-                                                                 const double* __restrict__ iq,
-                                                                 const double* __restrict__ abl,
-                                                                 uint16_t* __restrict__ rgb, CombOpt O) {
+template <class OPT>
+__device__ __forceinline__ void comb_out_row(const uint16_t* __restrict__ frames, const double* __restrict__ cvbuf,
+                                             const double* __restrict__ iq, const double* __restrict__ abl,
+                                             uint16_t* __restrict__ rgb, const OPT& O) {
   __shared__ uint16_t s_line[IN_X + 2];
   __shared__ uint16_t s_vbi[IN_X + 2];                   // -v: raw line l + 20 (the VBI copy, rows 20..23)
   __shared__ double s_y[IN_X];                           // AdjustY's Y (+ the VBI copy)
@@ -582,4 +608,19 @@ extern "C" __global__ __launch_bounds__(256) void ldg_k_comb_out(const uint16_t*
     out[x * 3 + 1] = (uint16_t)g;
     out[x * 3 + 2] = (uint16_t)b;
   }
+}
+
+extern "C" __global__ __launch_bounds__(256) void ldg_k_comb_out(const uint16_t* __restrict__ frames,
+                                                                 const double* __restrict__ cvbuf,
+                                                                 const double* __restrict__ iq,
+                                                                 const double* __restrict__ abl,
+                                                                 uint16_t* __restrict__ rgb) {
+  comb_out_row(frames, cvbuf, iq, abl, rgb, CombDefaults{});
+}
+extern "C" __global__ __launch_bounds__(256) void ldg_k_comb_out_opt(const uint16_t* __restrict__ frames,
+                                                                     const double* __restrict__ cvbuf,
+                                                                     const double* __restrict__ iq,
+                                                                     const double* __restrict__ abl,
+                                                                     uint16_t* __restrict__ rgb, CombOpt O) {
+  comb_out_row(frames, cvbuf, iq, abl, rgb, O);
 }

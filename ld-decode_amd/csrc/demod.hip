@@ -20,7 +20,6 @@
 #include "fft8k.hpp"
 #include "iir.hpp"
 #include "chan.hpp"
-#include "d05.hpp"
 
 using namespace ldg;
 
@@ -329,11 +328,11 @@ __device__ unsigned long long g_stamps[LDG_STAMP_BLOCKS][32];
       int64_t vchan_stride, double *__restrict__ audio1, int64_t aread_stride, int64_t achan_stride,              \
       int32_t *__restrict__ status, double2 *__restrict__ ospill, SyncTile *__restrict__ stiles,                 \
       double2 *__restrict__ aslice, double *__restrict__ sst, uint32_t *__restrict__ sbits,                      \
-      double4 *__restrict__ bst, double *__restrict__ d05halo, unsigned long long *__restrict__ span
+      double4 *__restrict__ bst, unsigned long long *__restrict__ span
 #define LDG_DEMOD_ARGS                                                                                            \
   smap, reads, cap, cap_first, cap_nsamp, fmt, tw, twk, rf_filt, g_video, g_05, iir, a_lfilt, a_rfilt, C, video, \
       vread_stride, vchan_stride, audio1, aread_stride, achan_stride, status, ospill, stiles, aslice, sst, sbits, \
-      bst, d05halo, span
+      bst, span
 __device__ __forceinline__ void demod_body(LDG_DEMOD_PARAMS) {
   __shared__ double2 s_x[M];          // 128 KiB: the 8192-point transforms
   __shared__ uint16_t s_bits[BLOCKLEN / 16];   // sync detector bits
@@ -672,13 +671,6 @@ __device__ __forceinline__ void demod_body(LDG_DEMOD_PARAMS) {
   STAMP(18);
   {
     const int t = fresh(tid);
-    if (t < D05_HALO && !kProbeNoStore) {
-      // the video samples demod_05's FIR window needs outside the kept range (d05.hpp):
-      // block positions [992, 1024) and [1024 + copylen, +32) mod 16384
-      const int p = t < 32 ? BLOCKCUT - 32 + t : (BLOCKCUT + copylen + (t - 32)) & (BLOCKLEN - 1);
-      const double2 z = sx[SWC(p >> 1)];
-      d05halo[((int64_t)slot * MAX_BLOCKS_PER_READ + b) * D05_HALO + t] = (p & 1) ? z.y : z.x;
-    }
     double x[IIR_CHUNK];
 #pragma unroll
     for (int c = 0; c < 8; c++) {

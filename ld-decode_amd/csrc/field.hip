@@ -16,7 +16,6 @@
 #include "field_rec.hpp"
 #include "pyops.hpp"
 #include "chan.hpp"
-#include "d05.hpp"
 
 using namespace ldg;
 
@@ -708,11 +707,8 @@ extern "C" __global__ __launch_bounds__(64) void ldg_k_linelocs(
 // crossing search and bad-line tests, one wave per line.  Writes the line's
 // refined location to LL2 and its flag to bad[] (0 ok, 1 bad, 2 the reference
 // raises on this line).  grid: n_reads * MAX_LINES workgroups of 64 threads.
-// demod_05 is not stored (d05.hpp): the wave rebuilds the window of it every
-// test below can touch, [s - 128, s + 576) around the line start s, in LDS;
-// a line whose window leaves the read evaluates the FIR per sample instead.
+// demod_05 is read from the channel the demod stores.
 namespace {
-constexpr int64_t HS_LO = 96, HS_HI = 544;    // calczc [s-1, s+401]; windows within [s-81, s+522]
 
 template <class Src>
 __device__ void hsync_line(const Src& d05, int64_t len, const SysConst& C, int i, double v, bool lb, int lane,
@@ -775,9 +771,8 @@ __device__ void hsync_line(const Src& d05, int64_t len, const SysConst& C, int i
 }  // namespace
 
 extern "C" __global__ __launch_bounds__(64) void ldg_k_hsync_lines(
-    const int32_t* __restrict__ smap, const ReadDesc* __restrict__ reads, const double* __restrict__ video,
-    int64_t vread_stride, int64_t vchan_stride, SysConst C, FieldRec* __restrict__ recs, double* __restrict__ lines,
-    int8_t* __restrict__ bad, const double* __restrict__ d05halo, const double* __restrict__ f05) {
+    const int32_t* __restrict__ smap, const double* __restrict__ video, int64_t vread_stride, int64_t vchan_stride,
+    SysConst C, FieldRec* __restrict__ recs, double* __restrict__ lines, int8_t* __restrict__ bad) {
   prio_latency();
 
   __shared__ double s_tmp[20];

@@ -42,8 +42,7 @@ constexpr int IIR_NPOW = 1025;
 constexpr int IIR_P1 = 16;
 constexpr int IIR_MB = IIR_P1 + 1040;
 constexpr int IIR_MP = IIR_MB + 4 * 1028;
-constexpr int IIR_F05 = IIR_MP + 4 * 1028;     // the 65 F05 taps (d05.hpp), padded to 72
-constexpr int IIR_TAB_N = IIR_F05 + 72;
+constexpr int IIR_TAB_N = IIR_MP + 4 * 1028;
 
 // Lane i of a wave reads x of another lane (DPP, no LDS round trip): CTRL
 // 0x111..0x118 = row_shr:1..8 (lane i - d of its row of 16, 0 below the row

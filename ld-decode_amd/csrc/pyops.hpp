@@ -167,7 +167,7 @@ __device__ inline int64_t wave_find_first(const Src& data, int64_t lo, int64_t h
 }
 
 // calczc above, wave-parallel search (same result and error semantics)
-// (Src: a pointer, or an indexable source such as d05.hpp's D05Src / D05Win)
+// (Src: a pointer or any indexable source)
 template <class Src>
 __device__ inline int wave_calczc(const Src& data, int64_t len, double start_offset, double target, int64_t count,
                                   int lane, double* res) {

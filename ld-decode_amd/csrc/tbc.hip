@@ -17,7 +17,6 @@
 #include "field_rec.hpp"
 #include "pyops.hpp"
 #include "chan.hpp"
-#include "d05.hpp"
 
 using namespace ldg;
 
@@ -794,22 +793,17 @@ __device__ __forceinline__ double* pilot_base(double* scratch, int slot) {
 }  // namespace
 
 // grid: n_reads * MAX_LINES workgroups of 64 threads (one wave per line): the
-// wave rebuilds demod_05 over the window (d05.hpp) and forms the flipped
-// (demod - demod_05) in LDS; lane 0 walks the crossings as the reference does.
+// wave forms the flipped (demod - demod_05) of the window in LDS; lane 0 walks
+// the crossings as the reference does.
 extern "C" __global__ __launch_bounds__(64) void ldg_k_pilot_lines(const int32_t* __restrict__ smap,
-                                                                   const ReadDesc* __restrict__ reads,
                                                                    const double* __restrict__ video,
                                                                    int64_t vread_stride, int64_t vchan_stride,
                                                                    SysConst C, FieldRec* __restrict__ recs,
                                                                    double* __restrict__ lines,
-                                                                   double* __restrict__ scratch,
-                                                                   const double* __restrict__ d05halo,
-                                                                   const double* __restrict__ f05) {
+                                                                   double* __restrict__ scratch) {
   prio_latency();
 
   constexpr int PW = 256;
-  __shared__ double s_vid[PW + 64];
-  __shared__ double s_d05[PW];
   __shared__ double s_pil[PW];
   const int lane = threadIdx.x;
   const int slot = smap[blockIdx.x / MAX_LINES];
@@ -821,7 +815,6 @@ extern "C" __global__ __launch_bounds__(64) void ldg_k_pilot_lines(const int32_t
   const double* ll = lines + (int64_t)slot * LINES_STRIDE + LL2 * MAX_LINES;
   const double* dm = video + (int64_t)slot * vread_stride + (int64_t)CH_DEMOD * vchan_stride;
   const int64_t len = R->n_out;
-  const D05Src d5(dm, d05halo, slot, f05, len, reads[slot].n_blocks);
   double* P = pilot_base(scratch, slot);
   double* offs = P + (int64_t)l * PILOT_MAX;
   double* meta = P + (int64_t)MAX_LINES * PILOT_MAX;    // [count, keep, median] per line

@@ -119,7 +119,7 @@ class RFTables:
                *burst_ba[0], *burst_ba[1][1:]]
         iir += ([*pilot_ba[0], *pilot_ba[1][1:]] if pilot_ba is not None else [0.0] * 5)
         self.tables['iir'] = np.array(iir, np.float64)
-        # the F05 taps: the library rebuilds demod_05 by this FIR where it is read (csrc/d05.hpp)
+        # the F05 taps: ldg_set_filters cross-checks fvideo05 == fvideo * DFT(taps)
         self.tables['f05_fir'] = np.asarray(f05_fir, np.float64)
 
         # audio (lddecode_core.py:223-279)

@@ -115,6 +115,29 @@ def test_gpu_comb_matches_oracle(gpu_ctx_ntsc):
 
 
 @pytest.mark.gpu
+def test_gpu_comb_default_kernels_equal_option_kernels(monkeypatch):
+    """At comb-ntsc's defaults the library runs comb kernels with the options folded in as
+    constants; the option-taking kernels (LDG_COMB_GENERIC=1, read at context creation)
+    must give the same rgb48 bit for bit."""
+    from ldgpu import native
+    from ldgpu.rfparams import RFTables
+    rf = RFTables('NTSC')
+    rng = np.random.default_rng(11)
+    noisy = frame_solid(45.0, 900, -400).astype(np.int64) + rng.integers(-400, 400, (525, 910))
+    noisy[:, :2] = frame_solid(45.0)[:, :2]
+    fr = np.stack([frame_solid(40.0, 1500, -900), np.clip(noisy, 0, 65535).astype(np.uint16)])
+    out = []
+    for generic in ('0', '1'):
+        monkeypatch.setenv('LDG_COMB_GENERIC', generic)
+        ctx = native.Context('NTSC', 0, max_reads=8)
+        ctx.set_filters(rf.params(), rf.tables)
+        ctx.comb_reset()
+        out.append(ctx.comb_ntsc(fr))
+        ctx.close()
+    assert np.array_equal(out[0], out[1])
+
+
+@pytest.mark.gpu
 def test_gpu_comb_on_decoded_frames():
     """RF -> .tbc on the GPU -> 2D comb on the GPU, against the oracle comb of the same
     frames (+-1 LSB) and the committed golden comb hashes (bit-exact frames reported)."""
