@@ -373,7 +373,7 @@ def main():
             dist.barrier()
 
     dec.ctx.profile(True if args.prof_all else 'demod')
-    reads0 = dec.stats['reads']
+    reads0, used0 = dec.stats['reads'], dec.stats['reads_used']
     barrier()
     t0 = time.perf_counter()
     frames = 0
@@ -399,6 +399,7 @@ def main():
     # figure a kernel trace of this command reports for ldg_k_demod_iso (profiles/)
     iso_reads, iso_ms = dec.demod_isolated(ISO_ITERS)
     reads_timed = dec.stats['reads'] - reads0
+    used_timed = dec.stats['reads_used'] - used0
     checks = wl.checks()
 
     if dist is not None:
@@ -423,11 +424,13 @@ def main():
     # fills the chip: one 150 KiB-LDS workgroup per CU).  Unit of work = one RF sample consumed;
     # algorithmic bytes per unit = SURVEY §8(d): input (1 B u8, 5/4 .lds, 4/3 .r30, 2 s16) +
     # .tbc out 955,500 / 1,334,667 B + .pcm 0.0048 B (1.7207 B for u8).  One launch of the
-    # roofline leg demodulates `iso_reads` field reads; a read yields consumed / reads_decoded
-    # new samples of the capture (reads overlap by ~1/3 and a few are speculative), so
-    # units per launch = iso_reads * consumed / reads_decoded over the timed steps.
+    # roofline leg demodulates `iso_reads` decoded field reads (FS_VALID: all their blocks
+    # inside the resident capture, so a sharded rank's out-of-window speculative reads
+    # are not among them); a field read the replay used advances the capture by
+    # consumed / reads_used samples (reads overlap by ~1/3), so
+    # units per launch = iso_reads * consumed / reads_used over the timed steps.
     bps = BYTES_PER_SAMPLE[args.fmt] + NTSC_TBC_BYTES_PER_SAMPLE + NTSC_PCM_BYTES_PER_SAMPLE
-    samples_per_read = consumed / max(reads_timed, 1)
+    samples_per_read = consumed / max(used_timed, 1)
     units_iso = iso_reads * samples_per_read
     achieved = bps * units_iso / (iso_ms * 1e-3) / 1e9
     traffic, lds = None, None
@@ -459,7 +462,8 @@ def main():
         'timing': ('isolated leg: %d launches of ldg_k_demod_iso over %d field reads (%d blocks) back to back, '
                    'HIP events on its stream; the kernel trace in profiles/ reports ldg_k_demod_iso per dispatch'
                    % (ISO_ITERS, iso_reads, iso_reads * READ_BLOCKS)),
-        'units_per_launch': round(units_iso), 'algorithmic_bytes_per_sample': round(bps, 4),
+        'units_per_launch': round(units_iso), 'samples_per_read': round(samples_per_read),
+        'algorithmic_bytes_per_sample': round(bps, 4),
         'algorithmic_bytes_per_launch': round(bps * units_iso),
         'traffic_unit': 'bytes per launch, 2*FETCH_SIZE + WRITE_SIZE (profiles/pmc_traffic.json, demod_iso)',
         'traffic_x_algorithmic': (traffic / (bps * units_iso)) if traffic else None,

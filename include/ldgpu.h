@@ -288,8 +288,10 @@ int ldg_sync(ldg_ctx* ctx);
  * on a PAL context the Y/C decoder of ldg_comb_pal, 576 x 1057 rgb48 per frame),
  * and copy the frames (and rgb48) to the host buffers asynchronously on the
  * output stream, overlapped with the next decode.  The buffers must stay valid
- * (pinned memory from ldg_host_alloc for full copy speed) until ldg_output_wait,
- * which waits for the last call's copies. */
+ * (pinned memory from ldg_host_alloc for full copy speed) until the matching
+ * ldg_output_wait: each call waits for the OLDEST outstanding ldg_output_async's
+ * copies (first in, first out; at most 4 outstanding, LDG_ESTATE past that), so
+ * the host can issue batch k+1 before handing batch k to its sink. */
 int ldg_output_async(ldg_ctx* ctx, int n, const int32_t* top_slots, const int32_t* bottom_slots, uint16_t* tbc_host,
                      uint16_t* rgb_host);
 int ldg_output_wait(ldg_ctx* ctx);

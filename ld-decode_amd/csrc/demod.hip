@@ -482,7 +482,11 @@ __device__ __forceinline__ void demod_body(LDG_DEMOD_PARAMS) {
       // threads (one that lands after the reload does not touch this block's data).
       // A mismatch flags the read and the host decodes it again (FS_MIGRATED).
       // (The round-3 form re-read the slot from the park in global memory: one
-      // memory latency per block.)
+      // memory latency per block.)  This is a HEURISTIC, not a proof: global stores
+      // to different addresses (different L2 channels) are not ordered, so a
+      // foreign wave's partial overwrite could land without its first slot and go
+      // undetected.  Migration needs compute-wave save/restore of a demod workgroup
+      // (a shared or oversubscribed GPU); every run so far reported 0 redos.
       const double2 pv = s_x[SW(slot_of(fresh(tid), 0).p)];
       if (park_sig(pv) != s_park_sig[tid]) status[slot] = FS_MIGRATED;
     }

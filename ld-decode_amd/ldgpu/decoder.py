@@ -442,8 +442,6 @@ class GPUDecoder:
         self.stats['reads'] += len(keys)
         self.pending.append((keys, slots))
         self.inflight.update(keys)
-        if len(keys) == self.batch:
-            self.wide_slots = list(slots)     # a full-width launch (bench.py's isolated roofline leg)
         return True
 
     def _launch_wait(self):
@@ -489,12 +487,17 @@ class GPUDecoder:
             h.append(best)
 
     def demod_isolated(self, iters=10):
-        """(reads, ms per launch) of the demod alone over the last full-width launch's reads,
-        `iters` launches back to back (the benchmark's roofline leg).  The reads' demod
+        """(reads, ms per launch) of the demod alone over `batch` decoded reads,
+        `iters` launches back to back (the benchmark's roofline leg).  The reads are the
+        most recent cached reads whose field decoded (FS_VALID): every block of such a
+        read lies inside the resident capture, so each launch demodulates whole reads
+        (a sharded rank's speculative reads past its window are FS_EOF and their
+        workgroups would return at once; the library refuses them).  The reads' demod
         outputs are recomputed in place, so the read cache is dropped."""
-        slots = getattr(self, 'wide_slots', None)
-        if not slots:
-            raise RuntimeError('no full-width launch to time')
+        slots = [sl for sl, inf in reversed(list(self.cache.values())) if inf.status == native.FS_VALID]
+        slots = slots[:self.batch]
+        if len(slots) < self.batch:
+            raise RuntimeError('demod_isolated: %d decoded reads cached, %d needed' % (len(slots), self.batch))
         ms = self.ctx.demod_isolated(slots, iters)
         self._reset_cache()
         return len(slots), ms
@@ -663,7 +666,8 @@ class GPUDecoder:
         return loader_tell(self.fmt, read_geometry(self.last_read)[2], self.cap_bytes)
 
     def decode(self, start_frame=0, length=None, sink=None, comb=False, comb_sink=None, start_sample=None,
-               stop_sample=None, keep_from=None, firstframe=True, archive=False, init_state=None, comb3d=None):
+               stop_sample=None, keep_from=None, firstframe=True, archive=False, init_state=None, comb3d=None,
+               resume=False):
         """Decode frames; sink(frame_u16, pcm_i16, meta) per frame (None: frames stay in HBM).
         The frame (and comb_sink's rgb48) handed to the sinks is a view of a pinned output
         buffer that a later batch reuses: copy it to keep it past the call.
@@ -681,23 +685,28 @@ class GPUDecoder:
         (lddecode.py:90); archive: keep each output field's audio inputs in the
         field archive instead of computing its 48 kHz audio (the shard's audio
         time offset is known only after the exchange), see self.shard_frames.
+        resume: continue the previous decode (same archive / shard_frames / audio-offset
+        transitions / comb state / fd.tell()) from start_sample, with the chain state in
+        init_state -- a shard extending its range past its nominal end (ShardedDecode.extend).
         Returns the number of frames decoded."""
         self.comb, self.comb_sink, self.comb3d = comb, comb_sink, (comb3d if comb else None)
         if self.comb3d is not None and sink is None:
             raise ValueError('the 3D comb runs on host frames (a sink is required)')
-        self.archive, self.arch_next, self.shard_frames = archive, 0, []
-        self.transitions = []
-        if comb:
-            self.ctx.comb_reset()
+        if not resume:
+            self.archive, self.arch_next, self.shard_frames = archive, 0, []
+            self.transitions = []
+            if comb:
+                self.ctx.comb_reset()
         spf = self.rf.samples_per_frame
         bpf = spf * 5 // 4                     # (sic) 10-bit packing assumed, lddecode.py:42
         size = self.cap_bytes
         if (size // bpf - start_frame) < 2:
             raise ValueError('start frame is past end of file')
         num_frames = length if length is not None else size // bpf - start_frame
-        self.mtf_level, self.audio_offset = 1, 0
-        self.last_framenr, self.last_isclv, self.last_read = None, False, None
-        self.frame_numbers, self.pcm_samples, self.last_meta = [], 0, None
+        if not resume:
+            self.mtf_level, self.audio_offset = 1, 0
+            self.last_framenr, self.last_isclv, self.last_read = None, False, None
+            self.frame_numbers, self.pcm_samples, self.last_meta = [], 0, None
         for k, v in (init_state or {}).items():        # chain state handed over by a previous shard
             setattr(self, k, v)
         nextsample = start_frame * spf if start_sample is None else start_sample
@@ -720,6 +729,9 @@ class GPUDecoder:
                 finally:
                     self._out_pending = None
                     self.ctx.sync()
+                    for ring in self._obufs or ():
+                        for b in ring:
+                            b.release_retired()
             finally:
                 if gc_on:
                     gc.enable()
@@ -846,14 +858,16 @@ class GPUDecoder:
             # frames (and the fused 2D comb) go to pinned host buffers asynchronously on the
             # output stream (ldg_output_async); the sink sees them at the next flush, after
             # ldg_output_wait -- no host round trip of the frames through the comb
+            rh, rw = (576, 1057) if self.sysp.name == 'PAL' else (self.ctx.comb_lines, 744)
             if self._obufs is None:
+                # two rings; one that grows keeps its old memory until the decode ends
+                # (the sink's views of it stay valid: PinnedBuffer.release_retired)
                 from .native import PinnedBuffer
                 self._obufs = [(PinnedBuffer(), PinnedBuffer()) for _ in range(2)]
             tb, rb = self._obufs[self._oring]
             self._oring ^= 1
             n = len(frames)
             pics = tb.view(n * H * W).reshape(n, H * W)
-            rh, rw = (576, 1057) if self.sysp.name == 'PAL' else (self.ctx.comb_lines, 744)
             rgb = rb.view(n * rh * rw * 3).reshape(n, rh, rw, 3) if self.comb else None
             self.ctx.output_async(tops, bots, pics, rgb)
             pics = (pics, rgb)

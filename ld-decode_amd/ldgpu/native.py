@@ -157,16 +157,22 @@ class LDGError(RuntimeError):
 
 
 class PinnedBuffer:
-    """Page-locked host memory (ldg_host_alloc) viewed as a numpy uint16 array; grows on demand."""
+    """Page-locked host memory (ldg_host_alloc) viewed as a numpy uint16 array; grows on
+    demand.  A grown buffer keeps its old allocation alive (retired) until
+    release_retired(): a view handed to a sink before the growth stays valid until the
+    owner says the views are dead (GPUDecoder.decode: at its end)."""
 
     def __init__(self):
         self.lib = load()
         self.ptr, self.nbytes, self.arr = None, 0, None
+        self.retired = []
 
     def view(self, count):
         nbytes = max(2 * count, 2)
         if nbytes > self.nbytes:
-            self.free()
+            if self.ptr is not None:
+                self.retired.append(self.ptr)
+            self.ptr, self.nbytes, self.arr = None, 0, None
             p = C.c_void_p()
             if self.lib.ldg_host_alloc(nbytes, C.byref(p)) != LDG_OK:
                 raise LDGError('ldg_host_alloc(%d) failed' % nbytes)
@@ -174,7 +180,13 @@ class PinnedBuffer:
             self.arr = np.ctypeslib.as_array(C.cast(p, C.POINTER(C.c_uint16)), shape=(nbytes // 2,))
         return self.arr[:count]
 
+    def release_retired(self):
+        for p in self.retired:
+            self.lib.ldg_host_free(p)
+        self.retired = []
+
     def free(self):
+        self.release_retired()
         if self.ptr is not None:
             self.lib.ldg_host_free(self.ptr)
             self.ptr, self.nbytes, self.arr = None, 0, None

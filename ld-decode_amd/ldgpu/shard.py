@@ -141,7 +141,10 @@ def decode_bounds(nsamples, nbytes, spf, world, start_frame=0, length=None, star
     count, ~80% of a u8 capture) are dropped, so the shards split only the samples
     the limit can reach -- the limit's nominal start plus two frames -- instead of
     the whole capture (whose last fifth a single decode never reads).  Every caller
-    (the decode, the capture windows, the benchmark) uses this one split."""
+    (the decode, the capture windows, the benchmark) uses this one split.  The split
+    is nominal (one frame per samples_per_frame): when skipped fields leave the ranks
+    short of the limit, the last rank reads on past its boundary (ShardedDecode.extend;
+    its capture window runs to the end of the capture)."""
     bpf = spf * 5 // 4
     limit = length if length is not None else nbytes // bpf - start_frame
     start = start_frame * spf if start_sample is None else start_sample
@@ -256,7 +259,7 @@ class ShardedDecode:
         comb with comb=True); nothing is spilled."""
         self.dec, self.rank, self.world = dec, rank, world
         self.resident, self.comb = resident, comb
-        self.whole_capture, self.window_misses = whole_capture, 0
+        self.whole_capture, self.window_misses, self.extended = whole_capture, 0, 0
         self.spf = dec.rf.samples_per_frame
         # the whole decode's frame count limit (lddecode.py:49; -l): frames past it are dropped
         self.bounds, self.limit, self.start = decode_bounds(dec.cap_nsamples, dec.cap_bytes, self.spf, world,
@@ -264,11 +267,17 @@ class ShardedDecode:
         self.warmup = warmup_frames
         self.frames = FrameSpill(spill_dir)   # this rank's output frames, in order
 
-    def _run(self, sink, start_sample, keep_from, firstframe, init=None):
-        dec = self.dec
+    def _stop(self):
         stop = self.bounds[self.rank + 1]
-        if self.rank == self.world - 1 and stop >= dec.cap_nsamples:
+        if self.rank == self.world - 1 and stop >= self.dec.cap_nsamples:
             stop = None
+        return stop
+
+    def _run(self, sink, start_sample, keep_from, firstframe, init=None, stop='nominal', length=None, resume=False):
+        """Decode [start_sample, stop) (stop 'nominal': this rank's boundary; None: no stop)."""
+        dec = self.dec
+        if stop == 'nominal':
+            stop = self._stop()
 
         def keep(pic, audio, meta):
             self.frames.append(pic)
@@ -276,15 +285,18 @@ class ShardedDecode:
                 sink(pic, None, meta)
 
         for attempt in range(2):
-            self.frames.reset()
+            if not resume:
+                self.frames.reset()
             try:
                 dec.decode(start_sample=start_sample, stop_sample=stop, keep_from=keep_from, firstframe=firstframe,
                            archive=True, sink=None if self.resident else keep, init_state=init,
-                           comb=self.comb)
+                           comb=self.comb, length=length, resume=resume)
                 return
             except WindowMiss:
                 # a read outside this rank's capture window: decode from the whole capture
-                if attempt or self.whole_capture is None:
+                # (not for a resumed decode: only the last rank resumes, and its window
+                # runs to the end of the capture)
+                if attempt or self.whole_capture is None or resume:
                     raise
                 self.whole_capture()
                 self.window_misses += 1
@@ -306,14 +318,47 @@ class ShardedDecode:
                 'first_mtf': sf[0]['mtf0'] if sf else None,
                 'last_next': sf[-1]['nextsample'] if sf else None,
                 'end_mtf': float(dec.mtf_level), 'end_framenr': dec.last_framenr, 'end_isclv': dec.last_isclv,
+                'end_read': dec.last_read,
                 'transitions': list(dec.transitions[t0:]), 't0': t0}
+
+    @staticmethod
+    def _state(s):
+        """The chain state a rank's summary hands to the next rank's first frame (the
+        framer's MTF / frame number / CLV flag, and fd.tell()'s read for the EOF guard)."""
+        return {'mtf_level': s['end_mtf'], 'last_framenr': s['end_framenr'], 'last_isclv': s['end_isclv'],
+                'last_read': s['end_read']}
 
     def refix(self, summaries, sink=None):
         """Re-decode from the previous rank's exact end state (chain mismatch)."""
         prev = next(s for s in reversed(summaries[:self.rank]) if s['n'])
-        self._run(sink, prev['last_next'], None, False,
-                  init={'mtf_level': prev['end_mtf'], 'last_framenr': prev['end_framenr'],
-                        'last_isclv': prev['end_isclv']})
+        self._run(sink, prev['last_next'], None, False, init=self._state(prev))
+        return self.summary()
+
+    def extend(self, summaries, sink=None):
+        """The last rank decodes on past its nominal end while the whole decode has fewer
+        frames than its limit.  The split assumes one frame per samples_per_frame; fields
+        the reference skips (invalid fields, "no/corrupt VSYNC found, jumping forward",
+        lddecode_core.py:909-920,1205-1212) move the limit's last frame later, and a single
+        decode reads as far as it takes (lddecode.py:88-90).  Returns the (possibly new)
+        summary, or None if nothing changed."""
+        if self.rank != self.world - 1:
+            return None
+        stop = self._stop()
+        base = frame_offsets(summaries)[self.rank]
+        me = summaries[self.rank]
+        want = self.limit - base - me['n']
+        if stop is None or want <= 0:
+            return None
+        if me['n']:
+            # the decoder still holds this rank's end state: continue from its last frame
+            self._run(sink, me['last_next'], None, False, stop=None, length=want, resume=True)
+        else:
+            # no frame of this rank's own: decode the rest from the previous rank's end state
+            prev = next((s for s in reversed(summaries[:self.rank]) if s['n']), None)
+            if prev is None:
+                return None
+            self._run(sink, prev['last_next'], None, False, init=self._state(prev), stop=None, length=want)
+        self.extended = len(self.dec.shard_frames) - me['n']
         return self.summary()
 
     def finish(self, summaries):
@@ -370,6 +415,9 @@ def decode_sharded(dec, rank, world, allgather, sink=None, start_frame=0, length
         summ = allgather(mine)
     if check_chain(summ):
         raise RuntimeError('sharded decode: chain did not converge')
+    # the last rank reads on while the decode is short of its frame limit (skipped fields)
+    ext = sd.extend(summ)
+    summ = allgather(ext if ext is not None else summ[rank])
     t2 = time.perf_counter()
     res = sd.finish(summ)
     if stats is not None:
@@ -377,6 +425,7 @@ def decode_sharded(dec, rank, world, allgather, sink=None, start_frame=0, length
             stats[k] = stats.get(k, 0.0) + v
         stats['refixes'] = stats.get('refixes', 0) + refixes
         stats['window_misses'] = stats.get('window_misses', 0) + sd.window_misses
+        stats['extended_frames'] = stats.get('extended_frames', 0) + sd.extended
         stats['frames_total'] = sum(s['n'] for s in summ)
     if resident:
         return [(g, None, a, m) for (g, a, m) in res]

@@ -78,3 +78,11 @@ def test_cli_drops_partial_block():
     got = np.frombuffer(r.stdout, dtype='<u2').reshape(-1, 2)
     assert got.shape == (3 * 1024, 2)
     assert np.array_equal(got, ocx.stream(data))
+
+
+@pytest.mark.gpu
+def test_native_matches_oracle_bit_exact_on_gpu_box():
+    """The same check in the GPU box's run (libldgpu.so as shipped there: the driver's
+    record of row F4); the expander itself is host code in the library."""
+    test_native_matches_oracle_bit_exact()
+    test_cli_drops_partial_block()

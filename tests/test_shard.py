@@ -50,6 +50,7 @@ class _FakeDec:
     def __init__(self, frames, mtf_level):
         self.shard_frames, self.mtf_level = frames, mtf_level
         self.transitions, self.last_framenr, self.last_isclv = [262] * len(frames), 12000, False
+        self.last_read = None
 
 
 def test_chain_check_uses_the_mtf_before_a_reread():
@@ -307,6 +308,164 @@ def test_sharded_window_miss_falls_back_to_whole_capture():
     assert len(got) == len(want)
     for (gf, ga, gm), (wf, wa, wm) in zip(got, want):
         assert gm == wm and np.array_equal(gf, wf) and np.array_equal(ga, wa)
+
+
+def run_ranks(sds):
+    """decode_sharded's phases for every rank of one process, one rank after another
+    (local decode -> chain check / refix -> the last rank's extension -> finish).
+    Returns [(global index, frame, pcm, meta)] in order and the summaries."""
+    summ = [sd.local() for sd in sds]
+    for _ in range(len(sds)):
+        bad = check_chain(summ)
+        if not bad:
+            break
+        summ = [sd.refix(summ) if r in bad else summ[r] for r, sd in enumerate(sds)]
+    assert check_chain(summ) == []
+    summ = [sd.extend(summ) or s for sd, s in zip(sds, summ)]
+    out = []
+    for sd in sds:
+        res = sd.finish(summ)
+        out += [(g, pic, a, m) for (g, a, m), pic in zip(res, sd.frames)]
+    return out, summ
+
+
+def windowed_decoders(data, fmt, system, world, batch=8, length=None):
+    """One GPUDecoder per rank holding the capture window shard_windows gives it (what
+    load_window leaves in HBM after the halo exchange), each with the whole-capture fallback."""
+    from ldgpu.decoder import GPUDecoder
+    from ldgpu.formats import samples_in_bytes
+    from ldgpu.shard import ShardedDecode
+    raw = np.frombuffer(bytes(data), np.uint8)
+    decs = [GPUDecoder(system=system, batch=batch) for _ in range(world)]
+    n = samples_in_bytes(fmt, raw.size)
+    spf = decs[0].rf.samples_per_frame
+    w = shard_windows(decode_bounds(n, raw.size, spf, world, length=length)[0], spf, n)
+    sds = []
+    for r, d in enumerate(decs):
+        lo, cut, hi = w[r]
+        b0 = sample_byte(fmt, lo)
+        b1 = raw.size if hi >= n else sample_byte(fmt, hi)
+        d.set_capture(raw[b0:b1], fmt, first_sample=lo, total_bytes=raw.size)
+        sds.append(ShardedDecode(d, r, world, length=length,
+                                 whole_capture=lambda d=d: d.set_capture(raw, fmt)))
+    return sds
+
+
+def assert_matches_oracle(got, frames, pcm, meta, pcm_sha=None):
+    """.tbc within +-1 LSB, .pcm bit-exact, metadata exact, frame for frame."""
+    import hashlib
+    assert [g for g, _, _, _ in got] == list(range(len(got)))
+    assert len(got) == len(frames), (len(got), len(frames))
+    for i, ((g, pic, a, m), f, p, om) in enumerate(zip(got, frames, pcm, meta)):
+        assert m == om, i
+        d = np.abs(np.asarray(pic, dtype=np.int64).reshape(-1) - f.astype(np.int64))
+        assert d.max() <= 1, (i, int(d.max()))
+        assert np.array_equal(a, p), i
+        if pcm_sha is not None:
+            assert hashlib.sha256(a.tobytes()).hexdigest() == pcm_sha[i]
+
+
+_ORACLE_1S = {}
+
+
+def _clv_1s():
+    """~1 s of NTSC CLV u8 RF and the oracle's decode of it (once per session)."""
+    if not _ORACLE_1S:
+        from ldgpu.synth import make_capture
+        from oracle.capture import FMT_U8
+        from oracle.framer import decode_capture
+        data = make_capture(int(40e6 * 1.0), 'u8', first_frame=3020, clv=True, seed=44)
+        _ORACLE_1S['v'] = (data,) + decode_capture(data, FMT_U8)
+    return _ORACLE_1S['v']
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('world', [2, 3, 4])
+@pytest.mark.parametrize('case', ['ntsc_clv_u8_0p2s', 'clv_1s'])
+def test_sharded_decode_vs_oracle(case, world):
+    """Config 5's decode (field-group sharded, capture windows, ranks one after another on
+    one device) against the ORACLE's single decode of the same capture -- not against
+    another GPU decode: .tbc +-1 LSB, .pcm bit-exact, per-frame metadata exact.  The golden
+    case's oracle output is itself pinned to the committed fixture's SHA-256s.  The chains
+    carried across the rank boundaries: read position, MTF, audio offset
+    (lddecode_core.py:1204,1289,1300-1309)."""
+    if case == 'clv_1s':
+        data, frames, pcm, meta = _clv_1s()
+        sys_, fmt, sha = 'NTSC', FMT_U8, None
+    else:
+        import sys
+        sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+        from test_gpu_parity import oracle_decode
+        from ldgpu.formats import NAME_TO_FMT
+        data, gold, frames, pcm, meta = oracle_decode(case)
+        sys_, fmt = gold['settings']['system'], NAME_TO_FMT[gold['settings']['fmt']]
+        sha = [g['pcm_sha256'] for g in gold['frames']]
+    sds = windowed_decoders(data, fmt, sys_, world)
+    got, summ = run_ranks(sds)
+    assert sum(1 for s in summ if s['n']) >= 2, [s['n'] for s in summ]     # really split
+    assert all(sd.window_misses == 0 for sd in sds)
+    assert_matches_oracle(got, frames, pcm, meta, sha)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('world', [2, 3])
+def test_sharded_skipped_fields_extend_the_last_rank(world):
+    """Fields the reference skips ("no/corrupt VSYNC found, jumping forward", 'not valid')
+    push the limit's last frame past the nominal split (the frame limit -l 5 here ends at
+    sample ~13.1 M, the split at 7 frames = 9.34 M): the last rank reads on past its
+    boundary, so the sharded decode still emits the reference's 5 frames."""
+    from ldgpu.synth import make_capture
+    from oracle.capture import FMT_U8
+    from oracle.framer import decode_capture
+    starts = [1052829 + int(k * 667333.5) for k in range(12)]
+    data = make_capture(int(40e6 * 0.5), 'u8', first_frame=300, seed=41,
+                        dropouts=tuple((s + 30000, 15000) for s in starts[2:10:2]))
+    frames, pcm, meta = decode_capture(data, FMT_U8, length=5)
+    spf = 1334668
+    assert len(frames) == 5 and meta[-1]['nextsample'] > 7 * spf      # past the nominal split
+    sds = windowed_decoders(data, FMT_U8, 'NTSC', world, length=5)
+    got, summ = run_ranks(sds)
+    assert sds[-1].extended > 0
+    assert_matches_oracle(got, frames, pcm, meta)
+
+
+@pytest.mark.gpu
+def test_sharded_300s_clv_8way_property():
+    """Config 5 at size (a 300 s CLV capture, 12 GB u8, field-sharded 8 ways on one device,
+    capture windows): consecutive CLV frame numbers across every rank boundary, the frame
+    count the reference's 10-bit EOF guard gives (lddecode.py:42,49,89), no chain re-fix
+    and no window miss."""
+    import torch
+    from ldgpu.decoder import GPUDecoder
+    from ldgpu.shard import ShardedDecode
+    n, world = int(40e6 * 300), 8
+    src = GPUDecoder(system='NTSC', batch=8)
+    src.ctx.synth(n, fmt=0, first_frame=1, clv=True, seed=23)
+    spf = src.rf.samples_per_frame
+    w = shard_windows(decode_bounds(n, n, spf, world)[0], spf, n)
+    sds, bufs = [], []
+    for r in range(world):
+        lo, cut, hi = w[r]
+        buf = torch.empty(hi - lo, dtype=torch.uint8, device='cuda')
+        src.ctx.capture_copy_to_device(buf.data_ptr(), lo, hi - lo)
+        torch.cuda.synchronize()
+        d = GPUDecoder(system='NTSC', batch=32)
+        d.set_capture(None, 0, device_ptr=buf.data_ptr(), nsamples=hi - lo, first_sample=lo, total_bytes=n)
+        bufs.append(buf)
+        sds.append(ShardedDecode(d, r, world, resident=True))
+    src.ctx.close()
+    summ = [sd.local() for sd in sds]
+    assert check_chain(summ) == []                     # no re-fix needed
+    summ = [sd.extend(summ) or s for sd, s in zip(sds, summ)]
+    nrs = []
+    for sd in sds:
+        res = sd.finish(summ)
+        nrs += [m['vbi']['framenr'] for _, _, m in res]
+        assert sd.window_misses == 0
+    bpf = spf * 5 // 4
+    assert len(nrs) == n // bpf, (len(nrs), n // bpf)
+    assert all(b == a + 1 for a, b in zip(nrs, nrs[1:]))
+    assert all(s['n'] > 0 for s in summ)
 
 
 def test_comb_start_state_matches_one_chain():
