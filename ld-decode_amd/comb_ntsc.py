@@ -24,11 +24,11 @@ stdout, as `comb-ntsc` does.  The options are the reference's getopt string
   -f       one file per frame, <-o base><framecode>.rgb (16-bit), nothing on stdout
   -o base  the -f file name base (default FRAME)
   -l line  black out line (line + 25) of the output
+  -W       910-wide output rows from x 0 instead of 744 from x 78 (a toggle, :974-976)
   -i file  input (default stdin)
 
--d 3 without -F (OpenCV Farneback optical flow), -W (910-wide output), -k
-(combk view), -D (2D debug), -t (training images) and -m (OpenCV monitor) are
-not built: they are rejected with a message rather than silently ignored.  A
+-d 3 without -F (OpenCV Farneback optical flow), -k (combk view), -D (2D
+debug), -t (training images) and -m (OpenCV monitor) are not built: they are rejected with a message rather than silently ignored.  A
 short final frame ends the stream like the reference's exit(0) (:1104,1114).
 Unknown options fail like the reference's getopt default (exit status 255).
 """
@@ -47,7 +47,7 @@ OUT_W = 744
 OPTSTRING = 'WQLakN:tFc:r:R:m8OwvDd:Bb:I:w:i:o:fphn:l:'     # comb-ntsc.cxx:972
 FRAME_INFO_CAV_EVEN, FRAME_INFO_CAV_ODD = 0x4, 0x8            # ld-decoder.h:247-252
 FRAME_INFO_WHITE_ODD, FRAME_INFO_WHITE_EVEN = 0x100, 0x200
-UNBUILT = {'-W': 'the 910-wide output (-W)', '-k': 'the combk view (-k)', '-D': 'the 2D debug mode (-D)',
+UNBUILT = {'-k': 'the combk view (-k)', '-D': 'the 2D debug mode (-D)',
            '-t': 'training mode (-t, OpenCV optical flow)', '-m': 'the OpenCV monitor (-m)'}
 
 
@@ -87,7 +87,9 @@ def parse(argv):
         if k in UNBUILT:
             print('ERROR: %s is not available in this build' % UNBUILT[k], file=sys.stderr)
             return 1
-        if k == '-L':
+        if k == '-W':
+            o['wide'] = not o.get('wide', False)
+        elif k == '-L':
             o['colorlpf'] = not o.get('colorlpf', True)
         elif k == '-Q':
             o['colorlpf_hq'] = not o.get('colorlpf_hq', True)
@@ -153,9 +155,9 @@ def read_frames(fh, n):
 class Writer:
     """PostProcess + WriteFrame (:894-938, :704-733) over the combed frames in order."""
 
-    def __init__(self, a, out, lines):
+    def __init__(self, a, out, lines, width=OUT_W):
         self.a, self.out, self.lines = a, out, lines
-        self.obuf = np.zeros((lines, OUT_W, 3), dtype=np.uint16)   # persists across frames (pulldown)
+        self.obuf = np.zeros((lines, width, 3), dtype=np.uint16)   # persists across frames (pulldown)
         self.oddframe, self.framecode = False, 0
 
     def write(self, obuf, fnum):
@@ -212,7 +214,7 @@ def main(argv=None):
     ctx.comb_reset()
     fin = open(a.infile, 'rb') if a.infile else sys.stdin.buffer
     out = sys.stdout.buffer
-    w = Writer(a, out, ctx.comb_lines)
+    w = Writer(a, out, ctx.comb_lines, ctx.comb_width)
     held = []                                  # 3D: the raw frames of outputs still to come
     while True:
         fr, last = read_frames(fin, a.chunk)

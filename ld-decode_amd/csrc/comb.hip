@@ -67,6 +67,10 @@ struct CombOpt {
   double black_ire;   // -I
   double bright_m;    // -b: brightness * 256 / 100
   double nr_y, nr_c;  // -n / -N times irescale; <= 0: DoYNR / DoCNR skipped
+  int wide;           // -W: 910-wide rows from x 0 (PostProcess rout_x / roffset, comb-ntsc.cxx:898-899);
+                      // nrows then covers every line DoYNR feeds (to 524) for its cross-line history
+  __host__ __device__ int out_w() const { return wide ? IN_X : OUT_W; }
+  __host__ __device__ int out_x0() const { return wide ? 0 : OUT_X0; }
   __host__ __device__ int iq_row0() const { return 44 - firstline; }               // first row with FilterIQ (line 44)
   __host__ __device__ int iq_rows() const { return nrows - iq_row0(); }
   __host__ __device__ int chain_lines() const { return IN_Y - firstline; }
@@ -80,6 +84,9 @@ struct CombDefaults {
   static constexpr int firstline = FIRST_LINE, nrows = OUT_H, out_rows = OUT_H;
   static constexpr int adaptive2d = 1, bw = 0, colorlpf = 1, lpq = 0, debug_row = -1;
   static constexpr double black_ire = 7.5, bright_m = 236.0 * 256 / 100, nr_y = 1.0 * IRESCALE, nr_c = 0.0;
+  static constexpr int wide = 0;
+  __host__ __device__ static constexpr int out_w() { return OUT_W; }
+  __host__ __device__ static constexpr int out_x0() { return OUT_X0; }
   __host__ __device__ static constexpr int iq_row0() { return 44 - firstline; }
   __host__ __device__ static constexpr int iq_rows() { return nrows - iq_row0(); }
   __host__ __device__ static constexpr int chain_lines() { return IN_Y - firstline; }
@@ -494,21 +501,52 @@ extern "C" __global__ __launch_bounds__(256) void ldg_k_comb_iq_opt(const double
 // threads (rows >= O.nrows are the -v frame's never-written bottom rows: 0).
 // For output pixels x >= 78 every FIR tap of DoYNR (h - 12 >= 66 >= 40) and
 // DoCNR (h + 12 - 16 >= 74 >= 60) falls inside the row, so their cross-line
-// histories never reach an output pixel.
+// histories never reach an output pixel.  With -W (x from 0) DoYNR's taps at
+// x 40..51 reach the previous fed line's last 12 feeds (positions 832..843 of
+// line l-1, or of line 524 of the previous frame -- of the previous call's last
+// frame through hist_in, 0 for the stream's first frame); DoCNR's reach only
+// positions 839..842 of the previous line, which are always 0 (FilterIQ writes
+// I / Q up to 837, AdjustY's held values past 840 are 0).
+
+// The Y DoYNR feeds at pixel p (40 <= p <= 843) of line L: AdjustY's (or the VBI
+// copy's) value, from the raw lines and L's signed-chroma row cv (comb-ntsc.cxx
+// :735-763, :870-877).
+__device__ __forceinline__ double fed_y(const uint16_t* __restrict__ fr, const double* __restrict__ cv, int L, int p) {
+  if (p >= 842) return 0.0;                              // untouched by AdjustY, never set by SplitIQ
+  if (L < 24 && p >= 4 && p < 840) return (double)fr[(size_t)(L + 20) * IN_X + p];
+  const uint16_t* line = fr + (size_t)L * IN_X;
+  const int q = p + 2;
+  const double yy = (L >= 36 && q >= 4 && q < 840) ? (double)line[q] : 0.0;
+  const double ii = held_i(cv, q), qq = held_q(cv, q);
+  double comp = 0;
+  switch (p & 3) {
+    case 0: comp = ii; break;
+    case 1: comp = -qq; break;
+    case 2: comp = -ii; break;
+    default: comp = qq; break;
+  }
+  if (line[0] == 16384) comp = -comp;
+  return yy + comp;
+}
+
 template <class OPT>
 __device__ __forceinline__ void comb_out_row(const uint16_t* __restrict__ frames, const double* __restrict__ cvbuf,
                                              const double* __restrict__ iq, const double* __restrict__ abl,
-                                             uint16_t* __restrict__ rgb, const OPT& O) {
+                                             uint16_t* __restrict__ rgb, const OPT& O,
+                                             const double* __restrict__ hist_in = nullptr,
+                                             double* __restrict__ hist_out = nullptr, int n = 0) {
   __shared__ uint16_t s_line[IN_X + 2];
   __shared__ uint16_t s_vbi[IN_X + 2];                   // -v: raw line l + 20 (the VBI copy, rows 20..23)
   __shared__ double s_y[IN_X];                           // AdjustY's Y (+ the VBI copy)
   __shared__ double s_i[IN_X], s_q[IN_X];                // FilterIQ's I / Q (DoCNR's input)
+  __shared__ double s_hist[12];                          // -W: the previous fed line's feeds 832..843
   const int tid = threadIdx.x;
   const int f = blockIdx.x / O.out_rows;
   const int row = blockIdx.x % O.out_rows;
-  uint16_t* out = rgb + ((size_t)f * O.out_rows + row) * OUT_W * 3;
+  const int W = O.out_w(), X0 = O.out_x0();
+  uint16_t* out = rgb + ((size_t)f * O.out_rows + row) * W * 3;
   if (row >= O.nrows) {
-    for (int x = tid; x < OUT_W * 3; x += 256) out[x] = 0;
+    for (int x = tid; x < W * 3; x += 256) out[x] = 0;
     return;
   }
   const int l = row + O.firstline;
@@ -525,6 +563,24 @@ __device__ __forceinline__ void comb_out_row(const uint16_t* __restrict__ frames
       s_vbi[2 * w + 1] = (uint16_t)(u >> 16);
     }
   }
+  if (O.wide) {
+    // DoYNR's history: the previous fed line (l - 1, or line 524 of the previous
+    // frame); the last row of the call's last frame hands its own feeds to the next call
+    const size_t fsz = (size_t)IN_X * IN_Y;
+    const int last = IN_Y - O.firstline - 1;             // the row of line 524 (nrows covers it with -W)
+    if (tid < 12) {
+      double v = 0.0;
+      if (row > 0)
+        v = fed_y(fr, cvbuf + ((size_t)f * O.nrows + row - 1) * CV_STRIDE, l - 1, 832 + tid);
+      else if (f > 0)
+        v = fed_y(fr - fsz, cvbuf + ((size_t)(f - 1) * O.nrows + last) * CV_STRIDE, IN_Y - 1, 832 + tid);
+      else if (hist_in)
+        v = hist_in[tid];
+      s_hist[tid] = v;
+    } else if (row == 0 && f == n - 1 && hist_out && tid >= 32 && tid < 44) {
+      hist_out[tid - 32] = fed_y(fr, cvbuf + ((size_t)f * O.nrows + last) * CV_STRIDE, IN_Y - 1, 832 + tid - 32);
+    }
+  }
   __syncthreads();
   const bool invertphase = (s_line[0] == 16384);
   const bool ycb = l >= 36;                              // SplitIQ sets cbuf's Y on lines 36..524 only
@@ -532,13 +588,16 @@ __device__ __forceinline__ void comb_out_row(const uint16_t* __restrict__ frames
   const bool fiq = O.colorlpf && l >= 44;
   const double* iqI = fiq ? iq + (((size_t)f * O.iq_rows() + (row - O.iq_row0())) * 2 + 0) * IQ_NS : nullptr;
   const double* iqQ = iqI ? iqI + IQ_NS : nullptr;
-  // I / Q at pixel t after FilterIQ (lines >= 44: I from feed (t - 2) / 2, Q from feed
-  // (t - 3) / 2), otherwise AdjustY's I / Q (the held values at t + 2)
-  auto I_at = [&](int t) { return iqI ? iqI[(t - 2) >> 1] : held_i(cv, t + 2); };
-  auto Q_at = [&](int t) { return iqQ ? iqQ[(t - 3) >> 1] : held_q(cv, t + 2); };
+  // I / Q at pixel t after FilterIQ (lines >= 44: I from feed (t - 2) / 2 for t in
+  // [2, 838), Q from feed (t - 3) / 2 for t in [3, 838)), otherwise AdjustY's I / Q
+  // (the held values at t + 2: 0 past 837 and before 2)
+  auto I_at = [&](int t) { return (iqI && t >= 2 && t < 838) ? iqI[(t - 2) >> 1] : held_i(cv, t + 2); };
+  auto Q_at = [&](int t) { return (iqQ && t >= 3 && t < 838) ? iqQ[(t - 3) >> 1] : (iqQ && t == 2) ? 0.0 : held_q(cv, t + 2); };
   // ---- AdjustY: p[h] = p[h + 2] with y += +-I / +-Q (h in [2, 842)); only
-  //      h in [66, 834) reaches an output pixel (DoYNR taps h-12..h+12)
-  for (int h = 66 + tid; h < 834; h += 256) {
+  //      h in [66, 834) reaches an output pixel (DoYNR taps h-12..h+12), all of
+  //      [0, 844) with -W (0 where AdjustY and SplitIQ leave the row alone)
+  const int ylo = O.wide ? 0 : 66, yhi = O.wide ? 844 : 834;
+  for (int h = ylo + tid; h < yhi; h += 256) {
     const int p = h + 2;
     const double yy = (ycb && p >= 4 && p < 840) ? (double)s_line[p] : 0.0;
     const double ii = held_i(cv, p), qq = held_q(cv, p);
@@ -550,12 +609,15 @@ __device__ __forceinline__ void comb_out_row(const uint16_t* __restrict__ frames
       default: comp = qq; break;
     }
     if (invertphase) comp = -comp;
-    s_y[h] = (vbi && h >= 4 && h < 840) ? (double)s_vbi[h] : yy + comp;
+    double v = (vbi && h >= 4 && h < 840) ? (double)s_vbi[h] : yy + comp;
+    if (h < 2 || h >= 842) v = 0.0;
+    s_y[h] = v;
   }
   if (O.nr_c > 0) {
-    for (int t = 74 + tid; t < 834; t += 256) {
-      s_i[t] = I_at(t);
-      s_q[t] = Q_at(t);
+    const int clo = O.wide ? 56 : 74, chi = O.wide ? 843 : 834;
+    for (int t = clo + tid; t < chi; t += 256) {
+      s_i[t] = t < 60 ? 0.0 : I_at(t);                   // t < 60: the previous line's feeds 839..842 (0)
+      s_q[t] = t < 60 ? 0.0 : Q_at(t);
     }
   }
   __syncthreads();
@@ -564,24 +626,31 @@ __device__ __forceinline__ void comb_out_row(const uint16_t* __restrict__ frames
   const double m = O.bright_m;
   const bool black = row == O.debug_row;
   const double kc = 10 / aburst, kb = 100 / (100 - O.black_ire);   // per-pixel factors of ToRGB, hoisted
-  for (int x = tid; x < OUT_W; x += 256) {
-    const int h = x + OUT_X0;
+  for (int x = tid; x < W; x += 256) {
+    const int h = x + X0;
     double yv = s_y[h];
-    if (O.nr_y > 0) {
+    // DoYNR on h in [40, 843); hplinef[h + 12] past the last feed (843) is 0
+    if (O.nr_y > 0 && (!O.wide || (h >= 40 && h + 12 <= 843))) {
       double y0 = 0;
 #pragma unroll
-      for (int o = 0; o < 25; o++) y0 += (g_nr.b[o] / 1.0) * s_y[h + 12 - o];
+      for (int o = 0; o < 25; o++) {
+        const int pp = h + 12 - o;
+        const double xv = (O.wide && pp < 40) ? s_hist[pp - 28] : s_y[pp];
+        y0 += (g_nr.b[o] / 1.0) * xv;
+      }
       double a = y0;
       if (fabs(a) > O.nr_y) a = (a > 0) ? O.nr_y : -O.nr_y;
       yv = s_y[h] - a;
     }
     double iv, qv;
-    if (O.nr_c > 0) {
+    if (O.nr_c > 0 && (!O.wide || (h >= 60 && h < 842))) {
       double ai = 0, aq = 0;
+      if (!O.wide || h + 12 <= 842) {
 #pragma unroll
-      for (int o = 0; o < 17; o++) {
-        ai += (g_nrc.b[o] / 1.0) * s_i[h + 12 - o];
-        aq += (g_nrc.b[o] / 1.0) * s_q[h + 12 - o];
+        for (int o = 0; o < 17; o++) {
+          ai += (g_nrc.b[o] / 1.0) * s_i[h + 12 - o];
+          aq += (g_nrc.b[o] / 1.0) * s_q[h + 12 - o];
+        }
       }
       if (fabs(ai) > O.nr_c) ai = (ai > 0) ? O.nr_c : -O.nr_c;
       if (fabs(aq) > O.nr_c) aq = (aq > 0) ? O.nr_c : -O.nr_c;
@@ -621,6 +690,8 @@ extern "C" __global__ __launch_bounds__(256) void ldg_k_comb_out_opt(const uint1
                                                                      const double* __restrict__ cvbuf,
                                                                      const double* __restrict__ iq,
                                                                      const double* __restrict__ abl,
-                                                                     uint16_t* __restrict__ rgb, CombOpt O) {
-  comb_out_row(frames, cvbuf, iq, abl, rgb, O);
+                                                                     uint16_t* __restrict__ rgb, CombOpt O,
+                                                                     const double* __restrict__ hist_in,
+                                                                     double* __restrict__ hist_out, int n) {
+  comb_out_row(frames, cvbuf, iq, abl, rgb, O, hist_in, hist_out, n);
 }

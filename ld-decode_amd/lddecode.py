@@ -52,7 +52,7 @@ def parse(argv=None):
     p.add_argument('--comb-3d-range', type=float, default=-1.0, help='comb-ntsc -r (IRE, default 5.5)')
     p.add_argument('--comb-args', default='',
                    help="comb-ntsc options for --comb (NTSC), e.g. '-I 0 -N 1 -v' (comb_ntsc.py's -I -b -n -N "
-                        "-B -a -L -Q -v -l)")
+                        "-B -a -L -Q -v -l -W)")
     p.add_argument('--no-json', action='store_true', help='do not write <outfile>.json')
     return p.parse_args(argv)
 
@@ -97,6 +97,9 @@ def main(argv=None):
         if isinstance(ca, int) or ca.write8 or ca.pulldown or ca.images or ca.oneframe or ca.dim != 2 or \
                 system != 'NTSC':
             print("ERROR: --comb-args takes comb-ntsc's arithmetic options (-I -b -n -N -B -a -L -Q -v -l), NTSC")
+            return 1
+        if world > 1 and ca.opts.get('wide'):
+            print("ERROR: a sharded decode does not hand comb-ntsc -W's cross-line Y-NR history across shards")
             return 1
         dec.ctx.comb_set_opts(**ca.opts)
     samples_per_frame = dec.rf.samples_per_frame                 # int(fs / FPS) + 1
@@ -240,7 +243,7 @@ def sharded(args, dec, outname, firstframe, num_frames, nextsample, req_frames, 
         pics = [pic for _, pic, _, _ in res]
         levels = allgather(comb_burst_levels(pics, line0=20 if dec.ctx.comb_lines == 525 else 38))
         dec.ctx.comb_set_state(comb_start_state(levels, rank))
-        rgb_bytes = 744 * dec.ctx.comb_lines * 3 * 2
+        rgb_bytes = dec.ctx.comb_width * dec.ctx.comb_lines * 3 * 2
         with open(outname + '.rgb', 'r+b') as fh:
             fh.seek(first * rgb_bytes)
             for i in range(0, len(pics), dec.ctx.max_frames):

@@ -858,7 +858,7 @@ class GPUDecoder:
             # frames (and the fused 2D comb) go to pinned host buffers asynchronously on the
             # output stream (ldg_output_async); the sink sees them at the next flush, after
             # ldg_output_wait -- no host round trip of the frames through the comb
-            rh, rw = (576, 1057) if self.sysp.name == 'PAL' else (self.ctx.comb_lines, 744)
+            rh, rw = (576, 1057) if self.sysp.name == 'PAL' else (self.ctx.comb_lines, self.ctx.comb_width)
             if self._obufs is None:
                 # two rings; one that grows keeps its old memory until the decode ends
                 # (the sink's views of it stay valid: PinnedBuffer.release_retired)

@@ -69,11 +69,11 @@ class CombOpts(C.Structure):
     """ldg_comb_opts (include/ldgpu.h): comb-ntsc's command-line options."""
     _fields_ = [('black_ire', C.c_double), ('brightness', C.c_double), ('nr_y', C.c_double), ('nr_c', C.c_double),
                 ('bw', C.c_int32), ('adaptive2d', C.c_int32), ('colorlpf', C.c_int32), ('colorlpf_hq', C.c_int32),
-                ('linesout', C.c_int32), ('debug_line', C.c_int32)]
+                ('linesout', C.c_int32), ('debug_line', C.c_int32), ('wide', C.c_int32)]
 
 
 COMB_DEFAULTS = dict(black_ire=7.5, brightness=236.0, nr_y=1.0, nr_c=0.0, bw=False, adaptive2d=True, colorlpf=True,
-                     colorlpf_hq=True, linesout=480, debug_line=-1000)
+                     colorlpf_hq=True, linesout=480, debug_line=-1000, wide=False)
 
 
 class Filters(C.Structure):
@@ -373,10 +373,11 @@ class Context:
         return a[:rc // a.itemsize]
 
     def comb_ntsc(self, frames):
-        """2D NTSC comb (comb-ntsc.cxx dim=2): n x (525, 910) uint16 frames -> n x (480, 744, 3) rgb48.
-        State (burst-level EMA) carries across calls like one reference comb process."""
+        """2D NTSC comb (comb-ntsc.cxx dim=2): n x (525, 910) uint16 frames -> n x (480, 744, 3) rgb48
+        (comb_lines x comb_width with -v / -W).  State (burst-level EMA, -W's Y-NR history)
+        carries across calls like one reference comb process."""
         f = np.ascontiguousarray(frames, dtype=np.uint16).reshape(-1, 525 * 910)
-        out = np.zeros((f.shape[0], self.comb_lines, 744, 3), dtype=np.uint16)
+        out = np.zeros((f.shape[0], self.comb_lines, self.comb_width, 3), dtype=np.uint16)
         self._check(self.lib.ldg_comb_ntsc(self.h, f.shape[0], f.ctypes.data_as(C.c_void_p),
                                            out.ctypes.data_as(C.c_void_p), 0), 'ldg_comb_ntsc')
         return out
@@ -385,7 +386,7 @@ class Context:
         """3D NTSC comb without optical flow (comb-ntsc -d 3 -F): n x (525, 910) uint16 frames in,
         the rgb48 frames that now have both neighbours out (none for a process's first two frames)."""
         f = np.ascontiguousarray(frames, dtype=np.uint16).reshape(-1, 525 * 910)
-        out = np.zeros((f.shape[0], self.comb_lines, 744, 3), dtype=np.uint16)
+        out = np.zeros((f.shape[0], self.comb_lines, self.comb_width, 3), dtype=np.uint16)
         n_out = C.c_int(0)
         self._check(self.lib.ldg_comb_ntsc3d(self.h, f.shape[0], f.ctypes.data_as(C.c_void_p),
                                              out.ctypes.data_as(C.c_void_p), C.byref(n_out), core_ire, range_ire),
@@ -444,6 +445,7 @@ class Context:
         self._check(self.lib.ldg_comb_set_state(self.h, float(aburstlev)), 'ldg_comb_set_state')
 
     comb_lines = 480                 # rows per rgb48 frame (comb-ntsc -v: 525)
+    comb_width = 744                 # pixels per rgb48 row (comb-ntsc -W: 910)
 
     def comb_set_opts(self, **opts):
         """comb-ntsc's options (ldg_comb_set_opts; keys of COMB_DEFAULTS, values as on the
@@ -456,6 +458,7 @@ class Context:
         c = CombOpts(**{k: (int(v) if isinstance(v, bool) else v) for k, v in o.items()})
         self._check(self.lib.ldg_comb_set_opts(self.h, C.byref(c)), 'ldg_comb_set_opts')
         self.comb_lines = int(o['linesout'])
+        self.comb_width = 910 if o['wide'] else 744
 
     def comb_reset(self):
         self._check(self.lib.ldg_comb_reset(self.h), 'ldg_comb_reset')

@@ -34,20 +34,20 @@ def _load():
 
 
 DEFAULT_OPTS = dict(black_ire=7.5, brightness=236.0, nr_y=1.0, nr_c=0.0, bw=False, adaptive2d=True,
-                    colorlpf=True, colorlpf_hq=True, linesout=480, debugline=-1000)
+                    colorlpf=True, colorlpf_hq=True, linesout=480, debugline=-1000, wide=False)
 
 
 def _set_opts(fn, h, opts):
     """comb-ntsc's options (comb-ntsc.cxx:972-1091): -I black_ire, -b brightness, -n nr_y,
-    -N nr_c (IRE), -B bw, -a / -L / -Q toggles, -v linesout 525, -l debugline."""
+    -N nr_c (IRE), -B bw, -a / -L / -Q toggles, -v linesout 525, -l debugline, -W wide."""
     o = dict(DEFAULT_OPTS)
     for k, v in opts.items():
         if k not in o:
             raise TypeError('unknown comb option %s' % k)
         o[k] = v
     d = np.array([o['black_ire'], o['brightness'], o['nr_y'], o['nr_c']], dtype=np.float64)
-    i = np.array([o['bw'], o['adaptive2d'], o['colorlpf'], o['colorlpf_hq'], o['linesout'], o['debugline']],
-                 dtype=np.int32)
+    i = np.array([o['bw'], o['adaptive2d'], o['colorlpf'], o['colorlpf_hq'], o['linesout'], o['debugline'],
+                  o['wide']], dtype=np.int32)
     fn(h, d.ctypes.data, i.ctypes.data)
     return o
 
@@ -68,7 +68,8 @@ class Comb2D:
 
     def process(self, frames):
         f = np.ascontiguousarray(frames, dtype=np.uint16).reshape(-1, IN_Y, IN_X)
-        out = np.zeros((f.shape[0], self.opts['linesout'], OUT_W, 3), dtype=np.uint16)
+        out = np.zeros((f.shape[0], self.opts['linesout'], IN_X if self.opts['wide'] else OUT_W, 3),
+                       dtype=np.uint16)
         self.lib.comb2d_process(self.h, f.shape[0], f.ctypes.data, out.ctypes.data)
         return out
 
@@ -94,7 +95,8 @@ class Comb3D:
 
     def process(self, frames):
         f = np.ascontiguousarray(frames, dtype=np.uint16).reshape(-1, IN_Y, IN_X)
-        out = np.zeros((f.shape[0], self.opts['linesout'], OUT_W, 3), dtype=np.uint16)
+        out = np.zeros((f.shape[0], self.opts['linesout'], IN_X if self.opts['wide'] else OUT_W, 3),
+                       dtype=np.uint16)
         n = self.lib.comb3d_process(self.h, f.shape[0], f.ctypes.data, out.ctypes.data, self.core, self.range)
         return out[:n]
 

@@ -31,7 +31,9 @@
 // Options (main's getopt, comb-ntsc.cxx:972-1091), struct Opts: -I black_ire,
 // -b brightness, -n nr_y, -N nr_c, -B b&w, -a (adaptive 2D off), -L (no colour
 // LPF), -Q (Q through colorlpq), -v (linesout 525: firstline 20, the VBI copy
-// shows), -l (debug line blacked out).  Output frames are 744 x linesout.
+// shows), -l (debug line blacked out), -W (910-wide output from x 0: PostProcess's
+// rout_x / roffset, :898-899; DoYNR's cross-line FIR history then reaches x 40..51).
+// Output frames are 744 (910 with -W) x linesout.
 #include <cmath>
 #include <cstdint>
 #include <algorithm>
@@ -77,7 +79,9 @@ const double NRC_B[17] = {
 // the options main() sets before Process runs (values as typed on the command line)
 struct Opts {
   double black_ire = 7.5, brightness = 236, nr_y = 1.0, nr_c = 0.0;
-  int bw = 0, adaptive2d = 1, colorlpf = 1, colorlpf_hq = 1, linesout = 480, debugline = -1000;
+  int bw = 0, adaptive2d = 1, colorlpf = 1, colorlpf_hq = 1, linesout = 480, debugline = -1000, wide = 0;
+  int out_w() const { return wide ? IN_X : OUT_W; }
+  int out_x0() const { return wide ? 0 : OUT_X0; }
 };
 
 struct YIQ { double y = 0, i = 0, q = 0; };
@@ -304,9 +308,11 @@ struct Comb {
         cb[l][h].q -= aq;
       }
     }
-    // ---- ToRGB + PostProcess: rows firstline.., x 78..821; rows past 524 - firstline stay 0 (-v)
+    // ---- ToRGB + PostProcess: rows firstline.., x 78..821 (0..909 with -W); rows past
+    //      524 - firstline stay 0 (-v)
     const double m = o.brightness * 256 / 100;
     const int out_h = o.linesout;
+    const int W = o.out_w(), X0 = o.out_x0();
     for (int l = FL; l < IN_Y; l++) {
       const double burstlev = raw[l * IN_X + 1] / IRESCALE;
       if (burstlev > 3) {
@@ -315,7 +321,7 @@ struct Comb {
       }
       const int row = l - FL;
       if (row >= out_h) continue;
-      for (int h = OUT_X0; h < OUT_X0 + OUT_W; h++) {
+      for (int h = X0; h < X0 + W; h++) {
         YIQ yiq = cb[l][h];
         yiq.i *= (10 / aburstlev);
         yiq.q *= (10 / aburstlev);
@@ -330,7 +336,7 @@ struct Comb {
         g = clampd(g * m, 0, 65535);
         b = clampd(b * m, 0, 65535);
         if (l == (o.debugline + 25)) r = g = b = 0;     // -l: the debug line is blacked out
-        uint16_t* op = rgb + ((size_t)row * OUT_W + (h - OUT_X0)) * 3;
+        uint16_t* op = rgb + ((size_t)row * W + (h - X0)) * 3;
         op[0] = (uint16_t)r;
         op[1] = (uint16_t)g;
         op[2] = (uint16_t)b;
@@ -345,17 +351,18 @@ extern "C" {
 void* comb2d_create() { return new Comb(); }
 void comb2d_destroy(void* c) { delete static_cast<Comb*>(c); }
 // the comb-ntsc options (doubles: black_ire, brightness, nr_y, nr_c; ints: bw, adaptive2d,
-// colorlpf, colorlpf_hq, linesout, debugline)
+// colorlpf, colorlpf_hq, linesout, debugline, wide)
 void comb2d_set_opts(void* c, const double* d, const int* i) {
   Opts& o = static_cast<Comb*>(c)->o;
   o.black_ire = d[0]; o.brightness = d[1]; o.nr_y = d[2]; o.nr_c = d[3];
   o.bw = i[0]; o.adaptive2d = i[1]; o.colorlpf = i[2]; o.colorlpf_hq = i[3]; o.linesout = i[4]; o.debugline = i[5];
+  o.wide = i[6];
 }
-// n frames of 910 x 525 uint16 -> n frames of 744 x linesout x 3 uint16 (rgb48)
+// n frames of 910 x 525 uint16 -> n frames of 744 (910 with -W) x linesout x 3 uint16 (rgb48)
 void comb2d_process(void* c, int n, const uint16_t* frames, uint16_t* rgb) {
   Comb* cb = static_cast<Comb*>(c);
   for (int f = 0; f < n; f++)
-    cb->process(frames + (size_t)f * IN_X * IN_Y, rgb + (size_t)f * OUT_W * cb->o.linesout * 3);
+    cb->process(frames + (size_t)f * IN_X * IN_Y, rgb + (size_t)f * cb->o.out_w() * cb->o.linesout * 3);
 }
 double comb2d_aburstlev(void* c) { return static_cast<Comb*>(c)->aburstlev; }
 
@@ -381,7 +388,7 @@ int comb3d_process(void* h, int n, const uint16_t* frames, uint16_t* rgb, double
   const int L = c->nhist + n;
   int out = 0;
   for (int k = 1; k + 1 < L; k++) {
-    c->c.process(&win[(size_t)k * F], rgb + (size_t)out * OUT_W * c->c.o.linesout * 3, &win[(size_t)(k - 1) * F],
+    c->c.process(&win[(size_t)k * F], rgb + (size_t)out * c->c.o.out_w() * c->c.o.linesout * 3, &win[(size_t)(k - 1) * F],
                  &win[(size_t)(k + 1) * F], core, range);
     out++;
   }

@@ -310,7 +310,9 @@ def test_cli_pal_comb(tmp_path):
                                            (['-d', '3', '-F', '-I', '0', '-b', '200'],
                                             dict(black_ire=0.0, brightness=200.0), 3),
                                            (['-d', '3', '-B', '-n', '0', '-Q', '-L'],
-                                            dict(bw=True, nr_y=0.0, colorlpf_hq=False, colorlpf=False), 2)])
+                                            dict(bw=True, nr_y=0.0, colorlpf_hq=False, colorlpf=False), 2),
+                                           (['-W', '-I', '0'], dict(wide=True, black_ire=0.0), 2),
+                                           (['-W', '-W'], dict(), 2)])
 def test_comb_cli_options_match_oracle(args, opts, dim):
     """comb_ntsc.py with the reference's option letters (the encode scripts' `-I 0`, CNR, -v,
     -b, -B forcing dim 2, the LPF toggles) against the oracle with the same options."""

@@ -426,7 +426,8 @@ def test_oracle_525_lines_and_debug_line():
 
 COMB_OPTION_CASES = [dict(black_ire=0.0), dict(black_ire=0.0, brightness=200.0), dict(nr_y=0.0), dict(nr_y=3.0),
                      dict(nr_c=2.0), dict(nr_c=0.5, nr_y=0.5), dict(bw=True), dict(linesout=525),
-                     dict(colorlpf=False), dict(colorlpf_hq=False), dict(adaptive2d=False), dict(debug_line=100)]
+                     dict(colorlpf=False), dict(colorlpf_hq=False), dict(adaptive2d=False), dict(debug_line=100),
+                     dict(wide=True), dict(wide=True, linesout=525, nr_c=1.0), dict(wide=True, nr_y=3.0)]
 
 
 def _opts_for_oracle(o):
@@ -451,6 +452,54 @@ def test_gpu_comb_options_match_oracle(gpu_ctx_ntsc, opts):
         ctx.comb_reset()
         g3 = ctx.comb_ntsc3d(fr)
         o3 = Comb3D(**_opts_for_oracle(opts)).process(fr)
+        assert g3.shape == o3.shape
+        assert np.abs(g3.astype(np.int64) - o3.astype(np.int64)).max() <= 1
+    finally:
+        ctx.comb_set_opts()
+        ctx.comb_reset()
+
+
+def test_oracle_wide_kat():
+    """-W (comb-ntsc.cxx:898-899, 974-976): 910-wide rows from x 0.  Columns 78..821 are the
+    744-wide output exactly; columns 0, 1 and 842..909 are black (AdjustY and SplitIQ leave
+    them 0 in cbuf, u16_to_ire(0) = -100 IRE, clamped to 0); DoYNR's cross-line history
+    reaches x 40..51 only: a different previous frame changes nothing else."""
+    fr = frames_3d(seed=21, n=3)
+    w = Comb2D(wide=True).process(fr)
+    n = Comb2D().process(fr)
+    assert w.shape == (3, 480, 910, 3)
+    assert np.array_equal(w[:, :, 78:822], n)
+    assert (w[:, :, 0:2] == 0).all() and (w[:, :, 842:] == 0).all()
+    # the history: the same frame after two different predecessors with the same burst
+    # levels (px 1: the global aburstlev chain stays the same)
+    # and a bright tail on its line 524; a wide Y-NR clip (-n 100) so the FIR's output shows
+    p1 = fr[0].copy()
+    p1[524, 820:840] = 60000
+    a = Comb2D(wide=True, nr_y=100.0).process(np.stack([fr[0], fr[2]]))[1]
+    b = Comb2D(wide=True, nr_y=100.0).process(np.stack([p1, fr[2]]))[1]
+    rows, cols = np.nonzero((a != b).any(axis=2))
+    assert cols.size and set(rows) == {0} and cols.min() >= 40 and cols.max() <= 51
+
+
+@pytest.mark.gpu
+def test_gpu_comb_wide_history_across_calls(gpu_ctx_ntsc):
+    """-W on the GPU in calls of 2 and 3 frames equals one oracle process over all 5 (+-1
+    LSB): DoYNR's history at x 40..51 enters from the previous frame, across the call
+    boundary through the context; 3D too."""
+    ctx, _ = gpu_ctx_ntsc
+    fr = frames_3d(seed=23, n=5)
+    fr[1, 524, 820:840] = 60000              # a bright tail the next frame's first row sees (x 40..51)
+    fr[2, 524, 820:840] = 60000
+    ctx.comb_set_opts(wide=True, nr_y=100.0)
+    try:
+        ctx.comb_reset()
+        g = np.concatenate([ctx.comb_ntsc(fr[:2]), ctx.comb_ntsc(fr[2:])])
+        o = Comb2D(wide=True, nr_y=100.0).process(fr)
+        assert g.shape == o.shape == (5, 480, 910, 3)
+        assert np.abs(g.astype(np.int64) - o.astype(np.int64)).max() <= 1
+        ctx.comb_reset()
+        g3 = np.concatenate([ctx.comb_ntsc3d(fr[:3]), ctx.comb_ntsc3d(fr[3:])])
+        o3 = Comb3D(wide=True, nr_y=100.0).process(fr)
         assert g3.shape == o3.shape
         assert np.abs(g3.astype(np.int64) - o3.astype(np.int64)).max() <= 1
     finally:
