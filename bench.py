@@ -39,6 +39,8 @@ if int(os.environ.get('GPU_MAX_HW_QUEUES', '0') or 0) < 12:
 NTSC_TBC_BYTES_PER_SAMPLE = 955500 / 1334667
 NTSC_PCM_BYTES_PER_SAMPLE = 0.0048
 NTSC_COMB_BYTES_PER_SAMPLE = (955500 + 2142720) / 1334667   # .tbc in + rgb48 out per frame
+PAL_TBC_BYTES_PER_SAMPLE = 1418750 / 1600000        # 1135 x 625 uint16 per 1.6 M samples
+PAL_COMB_BYTES_PER_SAMPLE = (1418750 + 1057 * 576 * 3 * 2) / 1600000
 BYTES_PER_SAMPLE = {0: 1.0, 1: 2.0, 2: 4 / 3, 3: 1.25}
 FMT_NAME = {0: 'u8', 1: 's16', 2: '10-bit .r30', 3: '10-bit .lds'}
 HBM_PEAK_GBS = 8000.0
@@ -67,9 +69,12 @@ def parse():
     # 128 had measured +1% (tools/batch_ab2.sh), before the clock settles
     ap.add_argument('--batch', type=int, default=96)
     ap.add_argument('--fmt', type=int, default=0, help='capture format: 0 u8, 1 s16, 2 .r30, 3 .lds (10-bit packed)')
+    ap.add_argument('--system', default='NTSC', choices=('NTSC', 'PAL'),
+                    help='PAL: config 3 (PAL CLV 40 MSPS u8, host-synthesised, the PAL Y/C decoder)')
     ap.add_argument('--clv', action='store_true',
                     help='CLV timecode instead of CAV picture numbers (captures past 79,999 frames, e.g. 1 h: config C5)')
-    ap.add_argument('--cpu-seconds', type=float, default=1.0, help='oracle baseline sample (seconds of RF)')
+    ap.add_argument('--cpu-frames', type=int, default=60,
+                    help='oracle baseline sample: frames per process (SURVEY §8(d): a 60-frame prefix)')
     ap.add_argument('--cpu-procs', type=int, default=0,
                     help='processes of the multi-process CPU baseline (default: the CPUs visible, at most 16)')
     ap.add_argument('--no-cpu', action='store_true')
@@ -83,22 +88,27 @@ def parse():
     return ap.parse_args()
 
 
-def _oracle_decode(data):
-    """One oracle decode (the numpy restatement of lddecode.py / lddecode_core.py), one core;
-    returns (RF samples consumed, frames, seconds)."""
+def _oracle_decode(data, fmt=0, system='NTSC', frames=None):
+    """One oracle decode (the numpy restatement of lddecode.py / lddecode_core.py), one core,
+    of the first `frames` frames (lddecode.py -l); returns (RF samples consumed, frames, seconds)."""
     from threadpoolctl import threadpool_limits
-    from oracle.capture import FMT_U8
     from oracle.framer import decode_capture
     # the oracle prints the reference's log lines ('not valid', ...): to stderr, so
     # the JSON line stays the only stdout output
     with threadpool_limits(limits=1), contextlib.redirect_stdout(sys.stderr):
         t0 = time.perf_counter()
-        frames, pcm, meta = decode_capture(bytes(data), FMT_U8)
+        out, pcm, meta = decode_capture(bytes(data), fmt, system=system, length=frames)
         dt = time.perf_counter() - t0
-    return (meta[-1]['nextsample'] if meta else 0), len(frames), dt
+    first = meta[0]['fields'][0]['readsample'] if meta else 0
+    return ((meta[-1]['nextsample'] - first) if meta else 0), len(out), dt
 
 
-SLICE_SHIFT = 170000          # about a quarter field of 40 MSPS NTSC RF
+SLICE_SHIFT = 170004          # about a quarter field of 40 MSPS RF (a multiple of 12: whole packing groups)
+
+
+def _sample_bytes(fmt, n):
+    """Bytes of n samples (n a multiple of 12) in a capture format."""
+    return {0: n, 1: 2 * n, 2: n // 3 * 4, 3: n // 4 * 5}[fmt]
 
 
 def _oracle_worker(args):
@@ -106,12 +116,12 @@ def _oracle_worker(args):
     as it stops the reference (vsync within the first 11 peaks, oracle/field.py); such a slice
     starts a quarter field later instead, as a sharded CPU runner would place its starts."""
     from oracle.demod import ReferenceCrash
-    path, off, n = args
+    path, off, nbytes, fmt, system, frames = args
     with open(path, 'rb') as fh:
         for j in range(4):
-            fh.seek(off + j * SLICE_SHIFT)
+            fh.seek(off + _sample_bytes(fmt, j * SLICE_SHIFT))
             try:
-                return _oracle_decode(fh.read(n))
+                return _oracle_decode(fh.read(nbytes), fmt, system, frames)
             except ReferenceCrash:
                 if j == 3:
                     raise
@@ -127,35 +137,51 @@ def cpu_model():
     return 'unknown'
 
 
-def cpu_baseline(capture, seconds, procs):
-    """The oracle on this box's host cores: (i) one process on one core, the
-    reference's own execution model (numpy FFT single-threaded), on the first `seconds` of the
-    benchmark's capture; (ii) `procs` processes at once, one core each, each on its own
-    `seconds` slice of the same capture (field-group sharding of the CPU path).  Bounded
-    samples, not the whole 60 s (about 16 s of CPU per second of RF)."""
+def cpu_sample_samples(system, frames):
+    """RF samples a `frames`-frame oracle decode needs: the 10-bit EOF guard
+    (lddecode.py:42,89) stops a capture of B bytes after ~B / (spf * 5 / 4) frames,
+    so the sample holds frames + 2 of those (a multiple of 12)."""
+    spf = 1600001 if system == 'PAL' else 1334668
+    return -(-((frames + 2) * (spf * 5 // 4)) // 12) * 12
+
+
+def cpu_baseline(get_capture, fmt, system, frames, procs):
+    """The oracle on this box's host cores: (i) one process on
+    one core, the reference's own execution model (numpy FFT single-threaded), over the first
+    `frames` frames of the benchmark's capture (lddecode.py -l frames); (ii) `procs`
+    processes at once, one core each, each over `frames` frames of its own slice of the same
+    capture (field-group sharding of the CPU path).  Bounded samples, not the whole capture
+    (about 16 s of CPU per second of RF).  get_capture(nbytes) -> the capture's first bytes."""
     import multiprocessing as mp
     import tempfile
-    n = int(40e6 * seconds)
-    consumed, nfr, dt = _oracle_decode(capture[:n])
+    n = cpu_sample_samples(system, frames)
+    nb = _sample_bytes(fmt, n)
+    consumed, nfr, dt = _oracle_decode(get_capture(nb), fmt, system, frames)
+    fname = {0: 'u8', 1: 's16', 2: '10-bit .r30', 3: '10-bit .lds'}[fmt]
     out = {'value': consumed / dt / 1e6, 'unit': 'RF Msamples/s', 'cores': 1, 'kind': 'port',
            'cpu_model': cpu_model(), 'host_cpus_visible': len(os.sched_getaffinity(0)),
-           'sample': ('the first %.2f s of the benchmark capture (synthetic NTSC u8 RF) -> %d frames through the '
-                      'oracle (numpy restatement of lddecode_core.py), %.1f s wall on 1 core' % (seconds, nfr, dt)),
+           'sample': ('the first %d frames of the benchmark capture (synthetic %s %s RF, lddecode.py -l %d) through '
+                      'the oracle (numpy restatement of lddecode_core.py:373-427,1193-1311), %.1f s wall on 1 core'
+                      % (nfr, system, fname, frames, dt)),
            'fields_per_s': 2 * nfr / dt}
-    if procs > 1 and capture.size >= procs * n + 3 * SLICE_SHIFT:
-        with tempfile.NamedTemporaryFile(prefix='ldg_cpu_', suffix='.u8') as fh:
-            fh.write(capture[:procs * n + 3 * SLICE_SHIFT].tobytes())
-            fh.flush()
-            ctx = mp.get_context('spawn')       # no inherited HIP state in the workers
-            t0 = time.perf_counter()
-            with ctx.Pool(procs) as pool:
-                res = pool.map(_oracle_worker, [(fh.name, k * n, n) for k in range(procs)])
-            wall = time.perf_counter() - t0
-        tot = sum(r[0] for r in res)
-        out['multi_process'] = {'value': tot / wall / 1e6, 'unit': 'RF Msamples/s', 'processes': procs,
-                                'cores': procs, 'fields_per_s': 2 * sum(r[1] for r in res) / wall,
-                                'sample': '%d x %.2f s slices of the benchmark capture, one process (one core) each, '
-                                          '%.1f s wall' % (procs, seconds, wall)}
+    total = _sample_bytes(fmt, procs * n + 3 * SLICE_SHIFT)
+    if procs > 1:
+        cap = get_capture(total)
+        if cap is not None and len(cap) >= total:
+            with tempfile.NamedTemporaryFile(prefix='ldg_cpu_') as fh:
+                fh.write(bytes(cap[:total]))
+                fh.flush()
+                ctx = mp.get_context('spawn')       # no inherited HIP state in the workers
+                t0 = time.perf_counter()
+                with ctx.Pool(procs) as pool:
+                    res = pool.map(_oracle_worker, [(fh.name, _sample_bytes(fmt, k * n), nb, fmt, system, frames)
+                                                    for k in range(procs)])
+                wall = time.perf_counter() - t0
+            tot = sum(r[0] for r in res)
+            out['multi_process'] = {'value': tot / wall / 1e6, 'unit': 'RF Msamples/s', 'processes': procs,
+                                    'cores': procs, 'fields_per_s': 2 * sum(r[1] for r in res) / wall,
+                                    'sample': '%d slices of the benchmark capture, %d frames each, one process '
+                                              '(one core) each, %.1f s wall' % (procs, frames, wall)}
     return out
 
 
@@ -211,6 +237,7 @@ class CaptureWorkload:
                 raise SystemExit('--host-io: u8 captures only')
             self.host_cap = dec.ctx.capture_download(0, self.nsamp)   # as a loader would hold it
         self.scaling = 'weak'
+        self.fmt, self.system = args.fmt, 'NTSC'
         self.data = 'synthetic (GPU-synthesised NTSC %s RF, %s)' % ('CLV' if args.clv else 'CAV', FMT_NAME[args.fmt])
 
     def step(self):
@@ -223,10 +250,11 @@ class CaptureWorkload:
             n = dec.decode(sink=None, comb=not args.no_comb)
         return n, dec.last_meta['nextsample']
 
-    def host_capture(self, n):
-        import numpy as np_
-        return self.host_cap[:n] if self.host_cap is not None else \
-            np_.asarray(self.dec.ctx.capture_download(0, min(n, self.nsamp)))
+    def host_capture(self, nbytes):
+        from ldgpu.formats import bytes_for_samples
+        nbytes = min(nbytes, bytes_for_samples(self.fmt, self.nsamp))
+        return self.host_cap[:nbytes] if self.host_cap is not None else \
+            np.asarray(self.dec.ctx.capture_download(0, nbytes))
 
     def config(self, frames):
         a = self.args
@@ -287,6 +315,7 @@ class ShardedWorkload:
         self.synth_s = time.perf_counter() - t0
         self.stats = {}
         self.scaling = 'strong'
+        self.fmt, self.system = 0, 'NTSC'
         self.data = 'synthetic (GPU-synthesised NTSC CLV RF, u8; each rank its window of one capture)'
         self.halo_rccl = False
 
@@ -318,10 +347,10 @@ class ShardedWorkload:
         first = res[0][3]['fields'][0]['readsample']
         return len(res), res[-1][3]['nextsample'] - first
 
-    def host_capture(self, n):
+    def host_capture(self, nbytes):
         if self.buf is not None:
-            return self.buf[:n].cpu().numpy()
-        return self.dec.ctx.capture_download(0, n)
+            return self.buf[:nbytes].cpu().numpy()
+        return self.dec.ctx.capture_download(0, nbytes)
 
     def config(self, frames):
         a = self.args
@@ -336,6 +365,44 @@ class ShardedWorkload:
                 'chain_refixes': self.stats.get('refixes', 0), 'window_misses': self.stats.get('window_misses', 0),
                 'halo_over_rccl': bool(self.halo_rccl),
                 'phase_s': {k: round(self.stats.get(k, 0.0), 4) for k in ('local_s', 'exchange_s', 'finish_s')}}
+
+
+class PALWorkload:
+    """configs[2]: PAL CLV, 40 MSPS u8 (10 s by default), synthesised on the
+    host (ldgpu/synth.py: PAL timing, 3.75 MHz pilot, CLV timecode) and made resident in HBM
+    before the timed region; one step decodes all of it RF -> .tbc + .pcm -> the PAL Y/C
+    decoder's rgb48 (row F2, build-defined), frames and rgb48 left in HBM."""
+
+    def __init__(self, args, dec, rank):
+        from ldgpu.synth import make_capture
+        self.args, self.dec = args, dec
+        self.nsamp = int(40e6 * (args.seconds or 10.0))
+        t0 = time.perf_counter()
+        self.raw = np.frombuffer(make_capture(self.nsamp, 'u8', system='PAL', clv=True, first_frame=3000,
+                                              seed=20181018 + rank), np.uint8)
+        dec.set_capture(self.raw, 0)
+        self.synth_s = time.perf_counter() - t0
+        self.scaling, self.fmt, self.system = 'weak', 0, 'PAL'
+        self.data = 'synthetic (host-synthesised PAL CLV RF, u8, 3.75 MHz pilot)'
+
+    def step(self):
+        dec = self.dec
+        dec._reset_cache()                           # fresh read cache: no reuse across steps
+        n = dec.decode(sink=None, comb=not self.args.no_comb)
+        return n, dec.last_meta['nextsample']
+
+    def host_capture(self, nbytes):
+        return self.raw[:nbytes]
+
+    def config(self, frames):
+        a = self.args
+        return {'workload': 'config 3: %g s PAL CLV, 40 MSPS u8 RF per GPU: RF->demod->TBC->.tbc+.pcm%s'
+                            % (self.nsamp / 40e6, '' if a.no_comb else '->PAL Y/C rgb48 (build-defined, row F2)'),
+                'frames_per_step': frames // max(a.steps, 1), 'batch_reads': a.batch, 'io': 'HBM-resident'}
+
+    def checks(self):
+        nrs = self.dec.frame_numbers
+        return {'framenr_consecutive': all(b == a + 1 for a, b in zip(nrs, nrs[1:]))}
 
 
 def main():
@@ -357,9 +424,12 @@ def main():
         dist = tdist
 
     from ldgpu.decoder import GPUDecoder
-    dec = GPUDecoder(system='NTSC', device=local, batch=args.batch)
-    sharded = args.sharded or (world > 1 and not args.independent)
-    wl = ShardedWorkload(args, dec, rank, world, dist) if sharded else CaptureWorkload(args, dec, rank)
+    dec = GPUDecoder(system=args.system, device=local, batch=args.batch)
+    sharded = args.system == 'NTSC' and (args.sharded or (world > 1 and not args.independent))
+    if args.system == 'PAL':
+        wl = PALWorkload(args, dec, rank)
+    else:
+        wl = ShardedWorkload(args, dec, rank, world, dist) if sharded else CaptureWorkload(args, dec, rank)
     progress(rank, 'capture synthesised (%.1f s)' % wl.synth_s)
 
     for w in range(args.warmup):
@@ -429,7 +499,9 @@ def main():
     # are not among them); a field read the replay used advances the capture by
     # consumed / reads_used samples (reads overlap by ~1/3), so
     # units per launch = iso_reads * consumed / reads_used over the timed steps.
-    bps = BYTES_PER_SAMPLE[args.fmt] + NTSC_TBC_BYTES_PER_SAMPLE + NTSC_PCM_BYTES_PER_SAMPLE
+    pal = args.system == 'PAL'
+    bps = BYTES_PER_SAMPLE[wl.fmt] + (PAL_TBC_BYTES_PER_SAMPLE if pal else NTSC_TBC_BYTES_PER_SAMPLE) + \
+        NTSC_PCM_BYTES_PER_SAMPLE
     samples_per_read = consumed / max(used_timed, 1)
     units_iso = iso_reads * samples_per_read
     achieved = bps * units_iso / (iso_ms * 1e-3) / 1e9
@@ -477,15 +549,16 @@ def main():
                              'consecutive launches; field kernels co-run on the CUs)'},
     }
     if not args.no_comb:
-        roofline['bytes_per_sample_with_comb'] = round(bps + NTSC_COMB_BYTES_PER_SAMPLE, 4)
+        roofline['bytes_per_sample_with_comb'] = round(bps + (PAL_COMB_BYTES_PER_SAMPLE if pal else
+                                                              NTSC_COMB_BYTES_PER_SAMPLE), 4)
     cpu = None
-    if not args.no_cpu and world == 1 and args.fmt == 0:
+    if not args.no_cpu and world == 1:
         # the capture in host memory, as a loader would read it (the CPU path's input)
         procs = args.cpu_procs or min(16, len(os.sched_getaffinity(0)))
-        cap = wl.host_capture(int(40e6 * args.cpu_seconds) * max(1, procs) + 3 * SLICE_SHIFT)
-        cpu = cpu_baseline(cap, args.cpu_seconds, procs)
+        progress(rank, 'CPU baseline (oracle, %d frames per process, 1 and %d processes)' % (args.cpu_frames, procs))
+        cpu = cpu_baseline(wl.host_capture, wl.fmt, wl.system, args.cpu_frames, procs)
     line = {
-        'metric': 'RF Msamples/s (40 MSPS NTSC, full RF->.tbc decode)', 'value': round(msps, 3),
+        'metric': 'RF Msamples/s (40 MSPS %s, full RF->.tbc decode)' % args.system, 'value': round(msps, 3),
         'unit': 'RF Msamples/s', 'n_gpus': world, 'steps': args.steps, 'warmup': args.warmup,
         'ms_per_step': round(dt_max / args.steps * 1e3, 3), 'higher_is_better': True, 'scaling': wl.scaling,
         'vs_baseline': None, 'dtype': 'f64', 'data': wl.data, 'config': wl.config(frames),

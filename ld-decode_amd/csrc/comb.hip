@@ -595,8 +595,8 @@ __device__ __forceinline__ void comb_out_row(const uint16_t* __restrict__ frames
   auto Q_at = [&](int t) { return (iqQ && t >= 3 && t < 838) ? iqQ[(t - 3) >> 1] : (iqQ && t == 2) ? 0.0 : held_q(cv, t + 2); };
   // ---- AdjustY: p[h] = p[h + 2] with y += +-I / +-Q (h in [2, 842)); only
   //      h in [66, 834) reaches an output pixel (DoYNR taps h-12..h+12), all of
-  //      [0, 844) with -W (0 where AdjustY and SplitIQ leave the row alone)
-  const int ylo = O.wide ? 0 : 66, yhi = O.wide ? 844 : 834;
+  //      of [0, 910) with -W (0 where AdjustY and SplitIQ leave the row alone)
+  const int ylo = O.wide ? 0 : 66, yhi = O.wide ? IN_X : 834;
   for (int h = ylo + tid; h < yhi; h += 256) {
     const int p = h + 2;
     const double yy = (ycb && p >= 4 && p < 840) ? (double)s_line[p] : 0.0;
