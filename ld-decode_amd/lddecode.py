@@ -215,12 +215,14 @@ def sharded(args, dec, outname, firstframe, num_frames, nextsample, req_frames, 
         print('rank %d: a read left the capture window; using the whole capture' % rank)
         dec.set_capture(raw, fmt)
 
-    # the rank's frames wait in a spill file beside the outputs until their global
-    # offsets are known (bounded host memory for any capture length)
+    # the rank's frames (and with --comb their rgb48, combed in HBM as they are decoded)
+    # wait in spill files beside the outputs until their global offsets are known
+    # (bounded host memory for any capture length)
+    stats = {}
     res = decode_sharded(dec, rank, world, allgather, start_frame=firstframe, length=num_frames,
                          start_sample=nextsample, whole_capture=whole,
-                         spill_dir=os.path.dirname(os.path.abspath(outname)))
-    sizes = allgather((len(res), sum(a.nbytes for _, _, a, _ in res)))
+                         spill_dir=os.path.dirname(os.path.abspath(outname)), comb=args.comb, stats=stats)
+    sizes = allgather((len(res), sum(r[2].nbytes for r in res)))
     frame_bytes = dec.sysp.outlinelen * dec.sysp.frame_lines * 2
     first = sum(n for n, _ in sizes[:rank])
     pcm_off = sum(b for _, b in sizes[:rank])
@@ -232,23 +234,22 @@ def sharded(args, dec, outname, firstframe, num_frames, nextsample, req_frames, 
     with open(outname + '.tbc', 'r+b') as tbc, open(outname + '.pcm', 'r+b') as pcm:
         tbc.seek(first * frame_bytes)
         pcm.seek(pcm_off)
-        for g, pic, audio, meta in res:
-            print('frame ', meta['vbi']['framenr'])
-            tbc.write(pic.tobytes())
-            pcm.write(audio.tobytes())
+        for r in res:
+            print('frame ', r[3]['vbi']['framenr'])
+            tbc.write(r[1].tobytes())
+            pcm.write(r[2].tobytes())
     if args.comb:
-        # the comb's burst-level EMA chains through every frame in order: each shard
-        # starts from the state the earlier shards' frames end in (exact, on the host)
-        from ldgpu.shard import comb_burst_levels, comb_start_state
-        pics = [pic for _, pic, _, _ in res]
-        levels = allgather(comb_burst_levels(pics, line0=20 if dec.ctx.comb_lines == 525 else 38))
-        dec.ctx.comb_set_state(comb_start_state(levels, rank))
+        # combed in HBM during the decode; the burst-level EMA (comb-ntsc.cxx:560-566,
+        # global over every frame) was handed across the ranks and the first frames
+        # re-combed with it (ldgpu/shard.py comb_fix)
+        print('rank %d: comb re-combed %d frame(s) with the exact burst-level state' %
+              (rank, stats.get('comb_recombed_frames', 0)))
         rgb_bytes = dec.ctx.comb_width * dec.ctx.comb_lines * 3 * 2
         with open(outname + '.rgb', 'r+b') as fh:
             fh.seek(first * rgb_bytes)
-            for i in range(0, len(pics), dec.ctx.max_frames):
-                fh.write(dec.ctx.comb_ntsc(np.stack(pics[i:i + dec.ctx.max_frames])).tobytes())
-    metas = allgather([m for _, _, _, m in res])
+            for r in res:
+                fh.write(np.ascontiguousarray(r[4]).tobytes())
+    metas = allgather([r[3] for r in res])
     total = sum(n for n, _ in sizes)
     if rank == 0:
         if req_frames is not None and total < req_frames:

@@ -229,6 +229,15 @@ class FrameSpill:
     def __len__(self):
         return self.n
 
+    def write_at(self, i, pic):
+        """Overwrite frame i (a re-combed frame)."""
+        pic = np.ascontiguousarray(pic)
+        assert pic.shape == self.shape and pic.dtype == self.dtype and 0 <= i < self.n
+        self._map = None
+        self.fh.seek(i * pic.nbytes)
+        self.fh.write(pic.tobytes())
+        self.fh.seek(0, 2)
+
     def __getitem__(self, i):
         if isinstance(i, slice):
             m = self._frames()
@@ -266,6 +275,10 @@ class ShardedDecode:
                                                             start_frame, length, start_sample)
         self.warmup = warmup_frames
         self.frames = FrameSpill(spill_dir)   # this rank's output frames, in order
+        # comb (CLI): the fused 2D comb's rgb48 frames, combed in HBM with the decode
+        # (ldg_output_async) from a "not initialised" burst-level EMA; comb_fix() then
+        # re-combs the first few with the exact state handed over from the earlier ranks
+        self.rgb = FrameSpill(spill_dir) if (comb and not resident) else None
 
     def _stop(self):
         stop = self.bounds[self.rank + 1]
@@ -287,10 +300,13 @@ class ShardedDecode:
         for attempt in range(2):
             if not resume:
                 self.frames.reset()
+                if self.rgb is not None:
+                    self.rgb.reset()
             try:
                 dec.decode(start_sample=start_sample, stop_sample=stop, keep_from=keep_from, firstframe=firstframe,
                            archive=True, sink=None if self.resident else keep, init_state=init,
-                           comb=self.comb, length=length, resume=resume)
+                           comb=self.comb, length=length, resume=resume,
+                           comb_sink=self.rgb.append if self.rgb is not None else None)
                 return
             except WindowMiss:
                 # a read outside this rank's capture window: decode from the whole capture
@@ -391,12 +407,44 @@ class ShardedDecode:
         return out
 
 
+def comb_fix(sd, allgather, nkept, stats=None):
+    """The comb's burst-level EMA across the ranks (comb-ntsc.cxx:560-566, global over
+    every frame): exchange each rank's chain summary, take the exact state entering this
+    rank, and re-comb (on the GPU) the first frames whose speculative state differed.
+    nkept: this rank's frames that are output (the frame limit may drop the rest).
+    Collective: every rank calls it."""
+    dec = sd.dec
+    line0 = 20 if dec.ctx.comb_lines == 525 else COMB_LINE0
+    lpf = 525 - line0
+    levels = comb_burst_levels(sd.frames[:nkept] if nkept else [], line0=line0)
+    summ = allgather(comb_summary(levels))
+    a0 = comb_start_from_summaries(summ, sd.rank)
+    full = a0 is None
+    if any(comb_start_from_summaries(summ, r) is None for r in range(len(summ))):
+        # some rank's chain had not converged within its prefix: exchange every level
+        every = allgather(levels)
+        a0, full = comb_start_state(every, sd.rank), True
+    k = comb_redo_frames(a0, levels, lpf)
+    if k:
+        dec.ctx.comb_set_state(a0)
+        for i in range(0, k, dec.ctx.max_frames):
+            j = min(k, i + dec.ctx.max_frames)
+            rgb = dec.ctx.comb_ntsc(np.stack([np.asarray(f) for f in sd.frames[i:j]]))
+            for q in range(j - i):
+                sd.rgb.write_at(i + q, rgb[q])
+    if stats is not None:
+        stats['comb_recombed_frames'] = stats.get('comb_recombed_frames', 0) + k
+        stats['comb_full_exchange'] = full
+    return k
+
+
 def decode_sharded(dec, rank, world, allgather, sink=None, start_frame=0, length=None, start_sample=None,
                    whole_capture=None, spill_dir=None, resident=False, comb=False, stats=None):
     """Run all phases with `allgather(obj) -> [obj per rank]` (torch.distributed
     all_gather_object, or an in-process stand-in).  Returns this rank's
-    [(global_index, frame, pcm, meta)]; the frames are memory-mapped views of the
-    rank's spill file (FrameSpill), valid while the returned list's frames are.
+    [(global_index, frame, pcm, meta)] (with comb: [(..., meta, rgb48)], the exact
+    comb output, comb_fix); the frames are memory-mapped views of the rank's spill
+    files (FrameSpill), valid while the returned list's frames are.
     resident: frames stay in HBM (benchmark mode) and frame is None."""
     import time
     t0 = time.perf_counter()
@@ -420,6 +468,8 @@ def decode_sharded(dec, rank, world, allgather, sink=None, start_frame=0, length
     summ = allgather(ext if ext is not None else summ[rank])
     t2 = time.perf_counter()
     res = sd.finish(summ)
+    if sd.rgb is not None:
+        comb_fix(sd, allgather, len(res), stats)
     if stats is not None:
         for k, v in (('local_s', t1 - t0), ('exchange_s', t2 - t1), ('finish_s', time.perf_counter() - t2)):
             stats[k] = stats.get(k, 0.0) + v
@@ -429,6 +479,8 @@ def decode_sharded(dec, rank, world, allgather, sink=None, start_frame=0, length
         stats['frames_total'] = sum(s['n'] for s in summ)
     if resident:
         return [(g, None, a, m) for (g, a, m) in res]
+    if sd.rgb is not None:
+        return [(g, pic, a, m, rgb) for (g, a, m), pic, rgb in zip(res, sd.frames, sd.rgb)]
     return [(g, pic, a, m) for (g, a, m), pic in zip(res, sd.frames)]
 
 
@@ -467,3 +519,55 @@ def comb_start_state(levels_by_rank, rank):
     for r in range(rank):
         a = comb_chain(a, levels_by_rank[r])
     return a
+
+
+# The EMA forgets: two runs over the same levels from different states differ by
+# 0.99^k after k qualifying lines and, once below an ulp, are the same double from
+# then on (csrc/comb.hip ldg_k_comb_burst).  A rank's chain over its frames is
+# therefore summarised by its first COMB_PREFIX levels, the state a run from "not
+# initialised" has after them and at the rank's end: a later rank replays the
+# prefix from the exact state entering the rank, and if that equals the
+# speculative state there, the exact state leaving the rank is the speculative
+# one.  ~12 frames' levels instead of every frame's (one hour on 8 ranks: 48 KB
+# per rank instead of 52 MB).
+COMB_PREFIX = 6144
+
+
+def comb_summary(levels):
+    """This rank's part of the comb chain exchange (see COMB_PREFIX)."""
+    levels = np.asarray(levels, dtype=np.float64)
+    if levels.size <= COMB_PREFIX:
+        return {'n': int(levels.size), 'levels': levels}
+    pre = levels[:COMB_PREFIX]
+    return {'n': int(levels.size), 'levels': pre, 'at_prefix': comb_chain(-1.0, pre),
+            'exit': comb_chain(-1.0, levels)}
+
+
+def comb_start_from_summaries(summaries, rank):
+    """The exact EMA entering `rank` from the earlier ranks' comb_summary()s, or None when
+    some rank's speculative chain had not met the exact one by the end of its prefix
+    (long stretches without burst: the caller then exchanges every level)."""
+    a = -1.0
+    for s in summaries[:rank]:
+        a = comb_chain(a, s['levels'])
+        if 'exit' in s:
+            if a != s['at_prefix']:
+                return None
+            a = s['exit']
+    return a
+
+
+def comb_redo_frames(a0, levels, lines_per_frame):
+    """How many of a rank's first frames the speculative comb (started "not
+    initialised") combed with a burst-level EMA other than the exact one (started
+    from a0): the frames before the first frame boundary where both states agree
+    (all of them if they never do)."""
+    levels = np.asarray(levels, dtype=np.float64)
+    nfr = levels.size // lines_per_frame
+    ex, sp = a0, -1.0
+    for f in range(nfr):
+        if ex == sp:
+            return f
+        part = levels[f * lines_per_frame:(f + 1) * lines_per_frame]
+        ex, sp = comb_chain(ex, part), comb_chain(sp, part)
+    return nfr

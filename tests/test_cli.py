@@ -219,6 +219,36 @@ def test_cli_sharded_two_ranks_equal_single(tmp_path):
 
 
 @pytest.mark.gpu
+def test_cli_sharded_fused_comb_recombs_only_the_first_frames(tmp_path):
+    """Three ranks with --comb on a 2 s capture: each rank combs its frames in HBM as they
+    are decoded (ldg_output_async) from a "not initialised" burst-level EMA, then re-combs
+    only its first frames with the exact state handed across the ranks (comb-ntsc.cxx:560-566;
+    ldgpu/shard.py comb_fix): the .rgb is byte-identical to one process's, and ranks 1 and 2
+    re-combed fewer frames than they hold."""
+    import re
+    import socket
+    from ldgpu.synth import make_capture
+    data = make_capture(int(40e6 * 2.0), 'u8', first_frame=900, seed=15)
+    cap = tmp_path / 'cap.u8'
+    cap.write_bytes(bytes(data))
+    r = run_cli('--comb', cap, tmp_path / 'one')
+    assert r.returncode == 0, r.stderr[-2000:]
+    with socket.socket() as sk:
+        sk.bind(('127.0.0.1', 0))
+        port = sk.getsockname()[1]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY='0')
+    r = subprocess.run([sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', '--nproc-per-node', '3',
+                        '--master-addr', '127.0.0.1', '--master-port', str(port), CLI, '--comb', str(cap),
+                        str(tmp_path / 'three')], capture_output=True, text=True, timeout=600, env=env)
+    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-3000:])
+    for ext in ('.tbc', '.pcm', '.rgb'):
+        assert (tmp_path / ('one' + ext)).read_bytes() == (tmp_path / ('three' + ext)).read_bytes(), ext
+    redo = {int(a): int(b) for a, b in re.findall(r'rank (\d+): comb re-combed (\d+) frame', r.stdout)}
+    nfr = len(json.load(open(tmp_path / 'one.json')))
+    assert redo.get(0) == 0 and 0 < redo[1] < nfr // 3 and 0 < redo[2] < nfr // 3, (redo, nfr)
+
+
+@pytest.mark.gpu
 def test_cli_sharded_rccl_halo_equal_single(tmp_path):
     """With a GPU per rank the capture-window halo travels between the GPUs' capture buffers
     over RCCL (lddecode.py load_window, ldgpu/shard.py exchange_halo): two ranks on two GPUs

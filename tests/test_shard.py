@@ -479,3 +479,30 @@ def test_comb_start_state_matches_one_chain():
     whole = comb_chain(-1.0, comb_burst_levels(frames[:3]))
     assert comb_start_state(lv, 2) == whole
     assert comb_start_state(lv, 0) == -1.0
+
+
+def test_comb_summaries_give_the_exact_start_state():
+    """The comb exchange of chain summaries (first COMB_PREFIX levels + the speculative
+    states) gives every rank the same start state as the full chain over all earlier
+    frames; a rank whose prefix has too few bursts to converge is reported (None)."""
+    from ldgpu.shard import (COMB_PREFIX, comb_chain, comb_redo_frames, comb_start_from_summaries,
+                             comb_start_state, comb_summary)
+    rng = np.random.default_rng(12)
+    lv = [rng.uniform(2.0, 25.0, n) for n in (3 * 487, 20 * 487, 15 * 487, 4 * 487)]
+    summ = [comb_summary(x) for x in lv]
+    for r in range(len(lv)):
+        assert comb_start_from_summaries(summ, r) == comb_start_state(lv, r)
+    quiet = np.concatenate([np.zeros(COMB_PREFIX + 10), rng.uniform(5, 20, 5000)])   # no burst at first
+    s2 = [summ[0], comb_summary(quiet), summ[2]]
+    assert comb_start_from_summaries(s2, 2) is None
+    # frames to re-comb: until the speculative chain (from "not initialised") meets the exact one
+    a0 = comb_start_state(lv, 2)
+    k = comb_redo_frames(a0, lv[2], 487)
+    assert 0 < k < 15
+    ex, sp = a0, -1.0
+    for f in range(15):
+        part = lv[2][f * 487:(f + 1) * 487]
+        if f >= k:
+            assert ex == sp
+        ex, sp = comb_chain(ex, part), comb_chain(sp, part)
+    assert comb_redo_frames(-1.0, lv[2], 487) == 0
