@@ -54,6 +54,12 @@ def parse(argv=None):
                    help="comb-ntsc options for --comb (NTSC), e.g. '-I 0 -N 1 -v' (comb_ntsc.py's -I -b -n -N "
                         "-B -a -L -Q -v -l -W)")
     p.add_argument('--no-json', action='store_true', help='do not write <outfile>.json')
+    p.add_argument('--epoch-frames', type=int, default=0,
+                   help='decode in epochs of N frames, each a complete (sharded) decode whose outputs are final '
+                        'before the next starts; with --manifest a crashed run resumes at the last finished epoch')
+    p.add_argument('--manifest', default=None,
+                   help='JSON progress manifest (epoch, frames and bytes written, the exact chain state): '
+                        'written after every epoch, read to resume')
     return p.parse_args(argv)
 
 
@@ -98,9 +104,6 @@ def main(argv=None):
                 system != 'NTSC':
             print("ERROR: --comb-args takes comb-ntsc's arithmetic options (-I -b -n -N -B -a -L -Q -v -l), NTSC")
             return 1
-        if world > 1 and ca.opts.get('wide'):
-            print("ERROR: a sharded decode does not hand comb-ntsc -W's cross-line Y-NR history across shards")
-            return 1
         dec.ctx.comb_set_opts(**ca.opts)
     samples_per_frame = dec.rf.samples_per_frame                 # int(fs / FPS) + 1
     bytes_per_frame = samples_per_frame * 5 // 4                 # for 10-bit packed files
@@ -133,8 +136,14 @@ def main(argv=None):
         return 0
 
     num_frames = req_frames if req_frames is not None else infile_size // bytes_per_frame - firstframe
-    if world > 1:
-        return sharded(args, dec, outname, firstframe, num_frames, nextsample, req_frames, raw, fmt, rccl)
+    if world > 1 or args.epoch_frames or args.manifest:
+        if args.comb and (system != 'NTSC' or args.comb_3d):
+            print("ERROR: a sharded or epoch-wise decode runs the 2D NTSC comb only")
+            return 1
+        if dec.ctx.comb_width != 744:
+            print("ERROR: a sharded or epoch-wise decode does not hand comb-ntsc -W's Y-NR history across pieces")
+            return 1
+        return sharded(args, dec, outname, firstframe, num_frames, nextsample, req_frames, raw, fmt, rccl, world)
     tbc = open(outname + '.tbc', 'wb')
     pcm = open(outname + '.pcm', 'wb')
     rgb = open(outname + '.rgb', 'wb') if args.comb else None
@@ -197,68 +206,142 @@ def load_window(dec, raw, fmt, rank, world, start, rccl, start_frame=0, length=N
     return buf
 
 
-def sharded(args, dec, outname, firstframe, num_frames, nextsample, req_frames, raw, fmt, rccl):
-    """This rank's share of a field-group sharded decode; every rank writes its frames
-    at their global offsets in the .tbc / .pcm, rank 0 writes the .json."""
-    import torch.distributed as dist
+def sharded(args, dec, outname, firstframe, num_frames, nextsample, req_frames, raw, fmt, rccl, world):
+    """This rank's share of a field-group sharded decode (any world size), in epochs of
+    --epoch-frames frames (default: one epoch).  Every rank writes its frames at their
+    global offsets in the .tbc / .pcm (/ .rgb); rank 0 writes the .json.  An epoch is a
+    complete decode: the next starts from the exact chain state after its last frame
+    (ShardedDecode.end_state), so the result equals one decode; with --manifest the
+    state is saved after every epoch and a rerun resumes after the last finished one."""
     from ldgpu.shard import decode_sharded
-    rank, world = dist.get_rank(), dist.get_world_size()
+    if world > 1:
+        import torch.distributed as dist
+        rank = dist.get_rank()
 
-    def allgather(obj):
-        out = [None] * world
-        dist.all_gather_object(out, obj)
-        return out
+        def allgather(obj):
+            out = [None] * world
+            dist.all_gather_object(out, obj)
+            return out
+        barrier = dist.barrier
+    else:
+        rank = 0
 
-    keep = load_window(dec, raw, fmt, rank, world, nextsample, rccl, firstframe, num_frames)   # noqa: F841
+        def allgather(obj):
+            return [obj]
+
+        def barrier():
+            pass
 
     def whole():
         print('rank %d: a read left the capture window; using the whole capture' % rank)
         dec.set_capture(raw, fmt)
 
-    # the rank's frames (and with --comb their rgb48, combed in HBM as they are decoded)
-    # wait in spill files beside the outputs until their global offsets are known
-    # (bounded host memory for any capture length)
-    stats = {}
-    res = decode_sharded(dec, rank, world, allgather, start_frame=firstframe, length=num_frames,
-                         start_sample=nextsample, whole_capture=whole,
-                         spill_dir=os.path.dirname(os.path.abspath(outname)), comb=args.comb, stats=stats)
-    sizes = allgather((len(res), sum(r[2].nbytes for r in res)))
-    frame_bytes = dec.sysp.outlinelen * dec.sysp.frame_lines * 2
-    first = sum(n for n, _ in sizes[:rank])
-    pcm_off = sum(b for _, b in sizes[:rank])
     exts = ('.tbc', '.pcm', '.rgb') if args.comb else ('.tbc', '.pcm')
-    if rank == 0:
-        for ext in exts:
-            open(outname + ext, 'wb').close()
-    dist.barrier()
-    with open(outname + '.tbc', 'r+b') as tbc, open(outname + '.pcm', 'r+b') as pcm:
-        tbc.seek(first * frame_bytes)
-        pcm.seek(pcm_off)
-        for r in res:
-            print('frame ', r[3]['vbi']['framenr'])
-            tbc.write(r[1].tobytes())
-            pcm.write(r[2].tobytes())
-    if args.comb:
-        # combed in HBM during the decode; the burst-level EMA (comb-ntsc.cxx:560-566,
-        # global over every frame) was handed across the ranks and the first frames
-        # re-combed with it (ldgpu/shard.py comb_fix)
-        print('rank %d: comb re-combed %d frame(s) with the exact burst-level state' %
-              (rank, stats.get('comb_recombed_frames', 0)))
-        rgb_bytes = dec.ctx.comb_width * dec.ctx.comb_lines * 3 * 2
-        with open(outname + '.rgb', 'r+b') as fh:
-            fh.seek(first * rgb_bytes)
+    parts = outname + '.json.part'             # one JSON line of frame metadata per finished epoch
+    man = None
+    if args.manifest and os.path.exists(args.manifest):
+        with open(args.manifest) as fh:
+            man = json.load(fh)
+        if man.get('infile_size') != os.path.getsize(args.infile) or man.get('exts') != list(exts) or \
+                man.get('num_frames') != num_frames:
+            print('ERROR: %s belongs to another decode' % args.manifest)
+            return 1
+        if rank == 0:
+            print('resuming after epoch %d (%d frames written)' % (man['epoch'], man['frames']))
+    if man is None:
+        man = {'infile_size': os.path.getsize(args.infile), 'exts': list(exts), 'num_frames': num_frames,
+               'epoch': 0, 'frames': 0, 'pcm_bytes': 0, 'state': None, 'nextsample': int(nextsample),
+               'complete': False}
+        if rank == 0:
+            for ext in exts:
+                open(outname + ext, 'wb').close()
+            open(parts, 'w').close()
+    elif rank == 0:
+        # drop a metadata line written after the manifest's last epoch (a crash in between)
+        with open(parts) as fh:
+            lines = fh.readlines()[:man['epoch']]
+        with open(parts, 'w') as fh:
+            fh.writelines(lines)
+    barrier()
+    frame_bytes = dec.sysp.outlinelen * dec.sysp.frame_lines * 2
+    rgb_bytes = dec.ctx.comb_width * dec.ctx.comb_lines * 3 * 2
+    epoch_frames = args.epoch_frames or num_frames
+    stats = {}
+    while not man['complete'] and man['frames'] < num_frames:
+        n = min(epoch_frames, num_frames - man['frames'])
+        keep = None
+        if world > 1:
+            keep = load_window(dec, raw, fmt, rank, world, man['nextsample'], rccl, firstframe, n)   # noqa: F841
+        ep = {}
+        # the rank's frames (and with --comb their rgb48, combed in HBM as they are decoded)
+        # wait in spill files beside the outputs until their global offsets are known
+        # (bounded host memory for any capture length)
+        res = decode_sharded(dec, rank, world, allgather, start_frame=firstframe, length=n,
+                             start_sample=man['nextsample'], whole_capture=whole,
+                             spill_dir=os.path.dirname(os.path.abspath(outname)), comb=args.comb, stats=stats,
+                             init=man['state'], epoch_end=ep)
+        sizes = allgather((len(res), sum(r[2].nbytes for r in res)))
+        first = man['frames'] + sum(k for k, _ in sizes[:rank])
+        pcm_off = man['pcm_bytes'] + sum(b for _, b in sizes[:rank])
+        with open(outname + '.tbc', 'r+b') as tbc, open(outname + '.pcm', 'r+b') as pcm:
+            tbc.seek(first * frame_bytes)
+            pcm.seek(pcm_off)
             for r in res:
-                fh.write(np.ascontiguousarray(r[4]).tobytes())
-    metas = allgather([r[3] for r in res])
-    total = sum(n for n, _ in sizes)
+                print('frame ', r[3]['vbi']['framenr'])
+                tbc.write(r[1].tobytes())
+                pcm.write(r[2].tobytes())
+        if args.comb:
+            # combed in HBM during the decode; the burst-level EMA (comb-ntsc.cxx:560-566,
+            # global over every frame) was handed across the ranks and the first frames
+            # re-combed with it (ldgpu/shard.py comb_fix)
+            print('rank %d: comb re-combed %d frame(s) with the exact burst-level state' %
+                  (rank, stats.get('comb_recombed_frames', 0)))
+            with open(outname + '.rgb', 'r+b') as fh:
+                fh.seek(first * rgb_bytes)
+                for r in res:
+                    fh.write(np.ascontiguousarray(r[4]).tobytes())
+        metas = allgather([r[3] for r in res])
+        total = sum(k for k, _ in sizes)
+        barrier()                                    # every rank's bytes of this epoch are written
+        man['epoch'] += 1
+        man['frames'] += total
+        man['pcm_bytes'] += sum(b for _, b in sizes)
+        man['state'] = ep or None
+        man['nextsample'] = ep.get('nextsample', man['nextsample'])
+        if total == 0 or not ep or total < n:
+            man['complete'] = True                   # end of the capture (the EOF guard or the limit)
+        if rank == 0:
+            with open(parts, 'a') as fh:
+                fh.write(json.dumps([m for part in metas for m in part]) + '\n')
+                fh.flush()
+                os.fsync(fh.fileno())
+            if args.manifest:
+                tmp = args.manifest + '.tmp'
+                with open(tmp, 'w') as fh:
+                    json.dump(man, fh)
+                os.replace(tmp, args.manifest)
+        barrier()
+        if int(os.environ.get('LDG_FAULT_AFTER_EPOCHS', '0') or 0) == man['epoch']:
+            print('rank %d: fault injected after epoch %d (LDG_FAULT_AFTER_EPOCHS)' % (rank, man['epoch']), flush=True)
+            os._exit(3)
     if rank == 0:
-        if req_frames is not None and total < req_frames:
+        if req_frames is not None and man['frames'] < req_frames:
             print('Warning: end of file reached before requested number of frames were decoded')
         if not args.no_json:
+            with open(parts) as fh:
+                allm = [m for line in fh for m in json.loads(line)]
             with open(outname + '.json', 'w') as fh:
-                json.dump([m for part in metas for m in part], fh)
-    dist.barrier()
-    dist.destroy_process_group()
+                json.dump(allm, fh)
+        os.remove(parts)
+        if args.manifest:
+            man['complete'] = True
+            with open(args.manifest + '.tmp', 'w') as fh:
+                json.dump(man, fh)
+            os.replace(args.manifest + '.tmp', args.manifest)
+    barrier()
+    if world > 1:
+        import torch.distributed as dist
+        dist.destroy_process_group()
     return 0
 
 

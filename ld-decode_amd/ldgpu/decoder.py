@@ -173,7 +173,7 @@ def field_log_lines(fields, ntsc):
 
 class FrameOut:
     __slots__ = ('top', 'bottom', 'audio_fields', 'vbi', 'nextsample', 'fields', 'index', 'start', 'tstart', 'mtf0',
-                 'log')
+                 'log', 'end')
 
     def __init__(self, **kw):
         for k, v in kw.items():
@@ -809,6 +809,8 @@ class GPUDecoder:
                 fr.start = nextsample
                 fr.tstart = cp[6]
                 fr.mtf0 = cp[1]                 # the MTF this frame's readframe began with (the chain state)
+                # the framer's state after this frame (the next decode's init: shard.py end_state)
+                fr.end = (self.mtf_level, self.last_framenr, self.last_isclv, self.last_read, len(self.transitions))
                 nextsample = fr.nextsample
                 if keep_from is not None and fr.start < keep_from:
                     continue                    # warm-up frame: chains only
@@ -896,7 +898,7 @@ class GPUDecoder:
                 self.shard_frames.append({'index': fr.index, 'start': int(fr.start), 'tstart': fr.tstart,
                                           'nextsample': int(fr.nextsample),
                                           'audio': ents, 'vbi': dict(fr.vbi), 'fields': fr.fields,
-                                          'mtf': float(fr.top.mtf_level), 'mtf0': float(fr.mtf0)})
+                                          'mtf': float(fr.top.mtf_level), 'mtf0': float(fr.mtf0), 'end': fr.end})
             self.arch_next += len(af)
             af = []
         # the audio runs while the host plans and replays the next batch: this batch's

@@ -45,6 +45,7 @@ from .decoder import WindowMiss, arange_last
 from .formats import FMT_LDS, FMT_R30, FMT_S16, FMT_U8
 
 GROUP = 12                      # window cuts on whole packing groups of every format (3 and 4 samples)
+CHAIN_KEYS = ('mtf_level', 'last_framenr', 'last_isclv', 'last_read')   # the framer state a decode continues from
 READ_SPAN = 1000001 + 2 * 16384  # a read's samples past its start (RFDecode.demod blocks)
 
 
@@ -175,9 +176,10 @@ def check_chain(summaries):
     return bad
 
 
-def start_offsets(summaries, line_period):
-    """Exact audio time offset at each rank's first frame (rank 0 starts at 0)."""
-    o, out = 0.0, []
+def start_offsets(summaries, line_period, o0=0.0):
+    """Exact audio time offset at each rank's first frame (rank 0 starts at o0: 0 at
+    the capture's start, the previous epoch's end offset for a later epoch)."""
+    o, out = o0, []
     for s in summaries:
         out.append(o)
         o = replay_offsets(o, s['transitions'], line_period)[-1]
@@ -260,13 +262,17 @@ class ShardedDecode:
     """One rank's part of a field-group sharded decode, in two phases."""
 
     def __init__(self, dec, rank, world, start_frame=0, warmup_frames=2, length=None, start_sample=None,
-                 whole_capture=None, spill_dir=None, resident=False, comb=False):
+                 whole_capture=None, spill_dir=None, resident=False, comb=False, init=None):
         """whole_capture: callable that makes the whole capture resident (the fallback
         when a capture window turns out too small).  spill_dir: where the output
         frames wait for the exchange (FrameSpill; default: the system temp dir).
         resident: the frames stay in HBM (benchmark mode: decode(sink=None), the fused
-        comb with comb=True); nothing is spilled."""
+        comb with comb=True); nothing is spilled.
+        init: the exact chain state at start_sample when it is not the capture's first
+        frame (a later epoch of an epoch-wise decode, epoch_state()): mtf_level,
+        last_framenr, last_isclv, last_read, audio_offset, comb_state, frame0."""
         self.dec, self.rank, self.world = dec, rank, world
+        self.init = init
         self.resident, self.comb = resident, comb
         self.whole_capture, self.window_misses, self.extended = whole_capture, 0, 0
         self.spf = dec.rf.samples_per_frame
@@ -321,7 +327,10 @@ class ShardedDecode:
         """Phase 1: decode this rank's range; returns the summary to exchange."""
         b = self.bounds[self.rank]
         if self.rank == 0:
-            self._run(sink, b, None, True)
+            if self.init is None:
+                self._run(sink, b, None, True)
+            else:
+                self._run(sink, b, None, False, init={k: self.init[k] for k in CHAIN_KEYS})
         else:
             self._run(sink, max(0, b - self.warmup * self.spf), b, False)
         return self.summary()
@@ -382,10 +391,11 @@ class ShardedDecode:
         Returns [(global_index, pcm int16, meta)] for this rank's frames."""
         dec = self.dec
         lp = dec.sysp.line_period
-        o0 = start_offsets(summaries, lp)[self.rank]
+        o0 = start_offsets(summaries, lp, self.init['audio_offset'] if self.init else 0.0)[self.rank]
         me = summaries[self.rank]
         offs = replay_offsets(o0, me['transitions'], lp)
         base = frame_offsets(summaries)[self.rank]
+        frame0 = self.init['frame0'] if self.init else 0
         ents = [(e, offs[t - me['t0']]) for f in dec.shard_frames for e, t in f['audio']]
         pcm_by_entry = {}
         step = dec.capacity
@@ -402,9 +412,33 @@ class ShardedDecode:
                 break
             parts = [pcm_by_entry[e] for e, _ in f['audio']]
             audio = np.concatenate(parts) if parts else np.zeros(0, dtype=np.int16)
-            meta = {'frame': base + i, 'vbi': f['vbi'], 'nextsample': f['nextsample'], 'fields': f['fields']}
+            meta = {'frame': frame0 + base + i, 'vbi': f['vbi'], 'nextsample': f['nextsample'], 'fields': f['fields']}
             out.append((base + i, audio, meta))
         return out
+
+    def end_state(self, summaries, comb_a0=None, line0=None):
+        """The exact chain state after the last frame the decode outputs (frame limit - 1,
+        or the last frame if fewer), if this rank holds that frame, else None: the next
+        epoch's init (an epoch-wise decode, lddecode.py --epoch-frames).  comb_a0: the
+        burst-level EMA entering this rank (comb_fix), run on over its frames up to that one."""
+        total = sum(s['n'] for s in summaries)
+        n = min(total, self.limit)
+        base = frame_offsets(summaries)[self.rank]
+        j = n - 1 - base
+        if n == 0 or not 0 <= j < summaries[self.rank]['n']:
+            return None
+        f = self.dec.shard_frames[j]
+        mtf, fnr, clv, last_read, tend = f['end']
+        o0 = self.init['audio_offset'] if self.init else 0.0
+        o = start_offsets(summaries, self.dec.sysp.line_period, o0)[self.rank]
+        me = summaries[self.rank]
+        o = replay_offsets(o, me['transitions'][:tend - me['t0']], self.dec.sysp.line_period)[-1]
+        comb = -1.0
+        if comb_a0 is not None:
+            comb = comb_chain(comb_a0, comb_burst_levels(self.frames[:j + 1], line0=line0))
+        return {'mtf_level': float(mtf), 'last_framenr': fnr, 'last_isclv': bool(clv),
+                'last_read': int(last_read), 'nextsample': int(f['nextsample']), 'audio_offset': float(o),
+                'comb_state': float(comb), 'frame0': (self.init['frame0'] if self.init else 0) + n}
 
 
 def comb_fix(sd, allgather, nkept, stats=None):
@@ -418,12 +452,13 @@ def comb_fix(sd, allgather, nkept, stats=None):
     lpf = 525 - line0
     levels = comb_burst_levels(sd.frames[:nkept] if nkept else [], line0=line0)
     summ = allgather(comb_summary(levels))
-    a0 = comb_start_from_summaries(summ, sd.rank)
-    full = a0 is None
-    if any(comb_start_from_summaries(summ, r) is None for r in range(len(summ))):
+    first = sd.init['comb_state'] if sd.init else -1.0          # the EMA entering the decode
+    a0 = comb_start_from_summaries(summ, sd.rank, first)
+    full = False
+    if any(comb_start_from_summaries(summ, r, first) is None for r in range(len(summ))):
         # some rank's chain had not converged within its prefix: exchange every level
         every = allgather(levels)
-        a0, full = comb_start_state(every, sd.rank), True
+        a0, full = comb_start_state(every, sd.rank, first), True
     k = comb_redo_frames(a0, levels, lpf)
     if k:
         dec.ctx.comb_set_state(a0)
@@ -435,21 +470,24 @@ def comb_fix(sd, allgather, nkept, stats=None):
     if stats is not None:
         stats['comb_recombed_frames'] = stats.get('comb_recombed_frames', 0) + k
         stats['comb_full_exchange'] = full
-    return k
+    return a0
 
 
 def decode_sharded(dec, rank, world, allgather, sink=None, start_frame=0, length=None, start_sample=None,
-                   whole_capture=None, spill_dir=None, resident=False, comb=False, stats=None):
+                   whole_capture=None, spill_dir=None, resident=False, comb=False, stats=None, init=None,
+                   epoch_end=None):
     """Run all phases with `allgather(obj) -> [obj per rank]` (torch.distributed
     all_gather_object, or an in-process stand-in).  Returns this rank's
     [(global_index, frame, pcm, meta)] (with comb: [(..., meta, rgb48)], the exact
     comb output, comb_fix); the frames are memory-mapped views of the rank's spill
     files (FrameSpill), valid while the returned list's frames are.
-    resident: frames stay in HBM (benchmark mode) and frame is None."""
+    resident: frames stay in HBM (benchmark mode) and frame is None.
+    init: the chain state at start_sample (a later epoch, ShardedDecode); epoch_end: a dict
+    that receives the exact state after the last output frame (ShardedDecode.end_state)."""
     import time
     t0 = time.perf_counter()
     sd = ShardedDecode(dec, rank, world, start_frame, length=length, start_sample=start_sample,
-                       whole_capture=whole_capture, spill_dir=spill_dir, resident=resident, comb=comb)
+                       whole_capture=whole_capture, spill_dir=spill_dir, resident=resident, comb=comb, init=init)
     loc = sd.local()
     t1 = time.perf_counter()
     summ = allgather(loc)
@@ -468,8 +506,14 @@ def decode_sharded(dec, rank, world, allgather, sink=None, start_frame=0, length
     summ = allgather(ext if ext is not None else summ[rank])
     t2 = time.perf_counter()
     res = sd.finish(summ)
+    a0 = None
     if sd.rgb is not None:
-        comb_fix(sd, allgather, len(res), stats)
+        a0 = comb_fix(sd, allgather, len(res), stats)
+    if epoch_end is not None:
+        # the exact state after the decode's last output frame (the next epoch's init)
+        ends = allgather(sd.end_state(summ, a0, 20 if dec.ctx.comb_lines == 525 else COMB_LINE0))
+        epoch_end.clear()
+        epoch_end.update(next((e for e in ends if e is not None), {}))
     if stats is not None:
         for k, v in (('local_s', t1 - t0), ('exchange_s', t2 - t1), ('finish_s', time.perf_counter() - t2)):
             stats[k] = stats.get(k, 0.0) + v
@@ -513,9 +557,9 @@ def comb_chain(a, levels):
     return a
 
 
-def comb_start_state(levels_by_rank, rank):
-    """The EMA a shard's comb starts from: the chain over every earlier shard's frames."""
-    a = -1.0
+def comb_start_state(levels_by_rank, rank, a=-1.0):
+    """The EMA a shard's comb starts from: the chain over every earlier shard's frames
+    (from a: -1, not initialised, at the capture's first frame)."""
     for r in range(rank):
         a = comb_chain(a, levels_by_rank[r])
     return a
@@ -543,11 +587,10 @@ def comb_summary(levels):
             'exit': comb_chain(-1.0, levels)}
 
 
-def comb_start_from_summaries(summaries, rank):
-    """The exact EMA entering `rank` from the earlier ranks' comb_summary()s, or None when
-    some rank's speculative chain had not met the exact one by the end of its prefix
-    (long stretches without burst: the caller then exchanges every level)."""
-    a = -1.0
+def comb_start_from_summaries(summaries, rank, a=-1.0):
+    """The exact EMA entering `rank` from the earlier ranks' comb_summary()s (from a at
+    rank 0), or None when some rank's speculative chain had not met the exact one by the
+    end of its prefix (long stretches without burst: the caller then exchanges every level)."""
     for s in summaries[:rank]:
         a = comb_chain(a, s['levels'])
         if 'exit' in s:

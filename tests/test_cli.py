@@ -249,6 +249,46 @@ def test_cli_sharded_fused_comb_recombs_only_the_first_frames(tmp_path):
 
 
 @pytest.mark.gpu
+def test_cli_epochs_resume_after_a_fault(tmp_path):
+    """--epoch-frames 7 --manifest: the decode runs as epochs that each start from the exact
+    chain state after the previous one's last frame (read position, MTF, frame number, the
+    EOF guard's read, 48 kHz offset, the comb's burst level): byte-identical to one decode.
+    A run killed after its second epoch (LDG_FAULT_AFTER_EPOCHS) resumes from the manifest
+    and ends with the same bytes; two ranks per epoch too."""
+    import socket
+    from ldgpu.synth import make_capture
+    data = make_capture(int(40e6 * 1.0), 'u8', first_frame=400, seed=16)
+    cap = tmp_path / 'cap.u8'
+    cap.write_bytes(bytes(data))
+    r = run_cli('--comb', cap, tmp_path / 'one')
+    assert r.returncode == 0, r.stderr[-2000:]
+    man = tmp_path / 'm.json'
+    env = dict(os.environ, LDG_FAULT_AFTER_EPOCHS='2')
+    r = subprocess.run([sys.executable, CLI, '--comb', '--epoch-frames', '7', '--manifest', str(man), str(cap),
+                        str(tmp_path / 'ep')], capture_output=True, text=True, timeout=600, env=env)
+    assert r.returncode == 3 and 'fault injected after epoch 2' in r.stdout, (r.stdout[-2000:], r.stderr[-2000:])
+    m = json.load(open(man))
+    assert m['epoch'] == 2 and m['frames'] == 14 and not m['complete']
+    r = run_cli('--comb', '--epoch-frames', '7', '--manifest', man, cap, tmp_path / 'ep')
+    assert r.returncode == 0 and 'resuming after epoch 2' in r.stdout, (r.stdout[-2000:], r.stderr[-2000:])
+    assert json.load(open(man))['complete']
+    for ext in ('.tbc', '.pcm', '.rgb'):
+        assert (tmp_path / ('one' + ext)).read_bytes() == (tmp_path / ('ep' + ext)).read_bytes(), ext
+    assert json.load(open(tmp_path / 'one.json')) == json.load(open(tmp_path / 'ep.json'))
+    with socket.socket() as sk:
+        sk.bind(('127.0.0.1', 0))
+        port = sk.getsockname()[1]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY='0')
+    r = subprocess.run([sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', '--nproc-per-node', '2',
+                        '--master-addr', '127.0.0.1', '--master-port', str(port), CLI, '--comb', '--epoch-frames', '9',
+                        str(cap), str(tmp_path / 'two')], capture_output=True, text=True, timeout=600, env=env)
+    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-3000:])
+    for ext in ('.tbc', '.pcm', '.rgb'):
+        assert (tmp_path / ('one' + ext)).read_bytes() == (tmp_path / ('two' + ext)).read_bytes(), ext
+    assert json.load(open(tmp_path / 'one.json')) == json.load(open(tmp_path / 'two.json'))
+
+
+@pytest.mark.gpu
 def test_cli_sharded_rccl_halo_equal_single(tmp_path):
     """With a GPU per rank the capture-window halo travels between the GPUs' capture buffers
     over RCCL (lddecode.py load_window, ldgpu/shard.py exchange_halo): two ranks on two GPUs
