@@ -215,6 +215,7 @@ class GPUDecoder:
         self.trace = None          # diagnostics: planner steps (tools/miss_probe.py)
         self.boot_wide = os.environ.get('LDG_BOOT_WIDE', '1') == '1'   # +6.5% on the 60 s bench (tools/bootwide_ab.sh)
         self.miss_drain = os.environ.get('LDG_MISS_DRAIN', '1') == '1'
+        self.grid_votes = int(os.environ.get('LDG_GRID_VOTES', '1'))   # _grid_next (1: the previous period's start)
         self.plan_located = 0              # leading fields the last plan walked on decoded reads
         self.htrace = [] if os.environ.get('LDG_HOSTTRACE') else None   # (perf_counter, event, n): host timeline
         self.comb, self.comb_sink = False, None
@@ -371,8 +372,8 @@ class GPUDecoder:
                         if h is not None:
                             nxt = h[0]
                         elif len(starts) >= self.period - 1:
-                            # r_{k+1} = r_{k+1-P} + D (P fields span D samples exactly)
-                            nxt = starts[-(self.period - 1)] + self.period_samples
+                            # r_{k+1} = r_{k+1-mP} + mD: P fields span D samples exactly
+                            nxt = self._grid_next(starts)
                         else:
                             nxt = key[0] + self.field_nom
                         valid = True
@@ -407,6 +408,27 @@ class GPUDecoder:
             firstframe = False
         self.plan_located = located
         return new, chain
+
+    def _grid_next(self, starts, votes=None):
+        """The next read start on the capture's field grid, r_{k+1} = r_{k+1-mP} + mD, voted
+        over m = 1..votes (the most common value; ties go to the smallest m).  A read start
+        is the absolute position of a sync peak found by argmax on a noisy channel
+        (lddecode_core.py:1204, Field.nextfieldoffset): grid + an independent +-1..2 sample
+        jitter (PAL: r[k+2] - r[k] = 1,600,000 +- 1 about one step in ten).  m = 1 alone
+        carries one jittered start into every P-th prediction after it (half of a 96-read
+        PAL launch wasted, profiles/r04_c_pal_waste_10s.txt); the vote keeps it to that read."""
+        P, D = self.period, self.period_samples
+        votes = votes or self.grid_votes
+        counts, best, bestc = {}, None, 0
+        for m in range(1, votes + 1):
+            j = m * P - 1
+            if j > len(starts):
+                break
+            c = starts[-j] + m * D
+            counts[c] = counts.get(c, 0) + 1
+            if counts[c] > bestc:
+                best, bestc = c, counts[c]
+        return best
 
     def _launch(self, keys, protect):
         """Decode `keys` now (launch and wait for everything outstanding)."""
@@ -818,7 +840,7 @@ class GPUDecoder:
                 fr.log = field_log_lines(self.field_log, self.sysp.name == 'NTSC') if self.frame_log else None
                 fr.index = done + len(frames)
                 frames.append(fr)
-                hist = (hist + [x.readsample for x in self.field_log if x.valid])[-16:]
+                hist = (hist + [x.readsample for x in self.field_log if x.valid])[-48:]
             self.stats['replay_s'] += time.perf_counter() - t0
             if self.stats['batches'] % 32 == 0:
                 gc.collect(1)

@@ -145,9 +145,11 @@ def run_decode(monkeypatch, frames, batch, jitter):
     return dec, n, nsamples
 
 
-@pytest.mark.parametrize('jitter', [False, True])
-def test_replay_matches_sequential_reference(monkeypatch, jitter):
-    """Batched speculative decode == the reference's sequential read chain (frames, numbers, end)."""
+@pytest.mark.parametrize('jitter,votes', [(False, 1), (True, 1), (True, 8)])
+def test_replay_matches_sequential_reference(monkeypatch, jitter, votes):
+    """Batched speculative decode == the reference's sequential read chain (frames, numbers, end),
+    with the planner's period prediction from the last period (votes 1) or voted over 8."""
+    monkeypatch.setenv('LDG_GRID_VOTES', str(votes))
     dec, n, nsamples = run_decode(monkeypatch, 300, batch=16, jitter=jitter)
     ref = reference_chain(nsamples)
     assert n == len(ref)
