@@ -245,6 +245,9 @@ typedef struct ldg_comb_opts {
   int32_t linesout;    /* 480; -v: 525 (from line 20: the VBI rows; the last 20 black) */
   int32_t debug_line;  /* -l  line (f_debugline + 25) blacked out; -1000 none        */
   int32_t wide;        /* -W  910-wide output rows from x 0 (default 0: 744 from 78) */
+  int32_t opticalflow; /* ldg_comb_ntsc3d: 1 = comb-ntsc -d 3 (with optical flow, the
+                          reference's default; BUILD-DEFINED Farneback),
+                          0 = -d 3 -F */
 } ldg_comb_opts;
 int ldg_comb_set_opts(ldg_ctx* ctx, const ldg_comb_opts* opts);
 /* Start the comb from a given burst-level EMA (comb-ntsc.cxx:560-566; -1 = not

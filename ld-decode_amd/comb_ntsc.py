@@ -8,8 +8,9 @@ Reads 910x525 uint16 .tbc frames from stdin (or -i) and writes rgb48 frames to
 stdout, as `comb-ntsc` does.  The options are the reference's getopt string
 "WQLakN:tFc:r:R:m8OwvDd:Bb:I:w:i:o:fphn:l:" with its meanings (:972-1068):
 
-  -d N     comb dimension, 2 (default) or 3 (needs -F, below)
-  -F       3D without optical flow; -c core / -r range (IRE, -F defaults 1.25 / 5.5)
+  -d N     comb dimension, 2 (default) or 3 (3D: optical flow, or -F)
+  -F       3D without optical flow; -c core / -r range (IRE; defaults 1.25 / 5.5 with -F,
+           0 / 0.5 with flow)
   -R x     p_3d2drej (parsed; the reference never uses it after main)
   -I ire   black level removed in the RGB conversion (default 7.5; encode-ntsc uses -I 0)
   -b x     brightness (default 236)
@@ -27,8 +28,11 @@ stdout, as `comb-ntsc` does.  The options are the reference's getopt string
   -W       910-wide output rows from x 0 instead of 744 from x 78 (a toggle, :974-976)
   -i file  input (default stdin)
 
--d 3 without -F (OpenCV Farneback optical flow), -k (combk view), -D (2D
-debug), -t (training images) and -m (OpenCV monitor) are not built: they are rejected with a message rather than silently ignored.  A
+-d 3 without -F (the reference's default) runs the 3D comb with optical flow:
+OpenCV's Farneback is absent here, so the flow is this build's restatement of it
+(csrc/flow.hip, oracle/farneback.py) -- BUILD-DEFINED, its parity with the
+reference unpinned.  -k (combk view), -D (2D debug), -t
+(training images) and -m (OpenCV monitor) are not built: they are rejected with a message rather than silently ignored.  A
 short final frame ends the stream like the reference's exit(0) (:1104,1114).
 Unknown options fail like the reference's getopt default (exit status 255).
 """
@@ -206,8 +210,11 @@ def main(argv=None):
         print('ERROR: -d must be 2 or 3 in this build', file=sys.stderr)
         return 1
     if a.dim == 3 and not a.no_of:
-        print('ERROR: -d 3 with optical flow (OpenCV Farneback) is not available; use -d 3 -F', file=sys.stderr)
-        return 1
+        if a.opts.get('wide'):
+            print('ERROR: -W with the optical-flow 3D comb is not built (the flow path feeds the Y-NR '
+                  'history -W shows); use -d 3 -F -W', file=sys.stderr)
+            return 1
+        a.opts['opticalflow'] = True
     from ldgpu import native
     ctx = native.Context('NTSC', a.device, max_reads=1, max_frames=a.chunk)
     ctx.comb_set_opts(**a.opts)

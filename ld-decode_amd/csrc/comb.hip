@@ -67,6 +67,7 @@ struct CombOpt {
   double black_ire;   // -I
   double bright_m;    // -b: brightness * 256 / 100
   double nr_y, nr_c;  // -n / -N times irescale; <= 0: DoYNR / DoCNR skipped
+  int of;             // ldg_comb_ntsc3d with optical flow (comb-ntsc -d 3 without -F; host only)
   int wide;           // -W: 910-wide rows from x 0 (PostProcess rout_x / roffset, comb-ntsc.cxx:898-899);
                       // nrows then covers every line DoYNR feeds (to 524) for its cross-line history
   __host__ __device__ int out_w() const { return wide ? IN_X : OUT_W; }
@@ -301,10 +302,14 @@ extern "C" __global__ __launch_bounds__(256) void ldg_k_comb_burst(const uint16_
 // ---- ldg_k_comb_split: SplitIQ's signed chroma of one row.
 // grid: n * O.nrows workgroups of 256 threads; row r = line r + firstline; cv: [n][nrows][CV_STRIDE].
 // D3: frames[f] has its neighbours at frames[f -+ 1] (core / range: p_3dcore,
-// p_3drange times irescale).
-template <bool D3, class OPT>
+// p_3drange times irescale).  OF (with D3): the 3D mode with optical flow
+// (Split3D(f, true), comb-ntsc.cxx:395-407): clp2 = next - cur and combk[2] from the
+// flow's weight map kmap[f] (252 x 840 per frame: frame rows 2 y, 2 y + 1, columns
+// 70..909; 0 elsewhere; flow.hip ldg_k_flow_combk).
+template <bool D3, class OPT, bool OF = false>
 __device__ __forceinline__ void comb_split_row(const uint16_t* __restrict__ frames, double* __restrict__ cvbuf,
-                                               double core, double range, const OPT& O) {
+                                               double core, double range, const OPT& O,
+                                               const double* __restrict__ kmap = nullptr) {
   __shared__ uint16_t s_raw[3][IN_X + 2];                // raw lines l-2, l, l+2
   __shared__ double s_c[3][IN_X];                        // Split1D clp0 of those lines
   __shared__ uint16_t s_pn[D3 ? 2 : 1][IN_X + 2];        // 3D: line l of the previous / next frame
@@ -339,7 +344,7 @@ __device__ __forceinline__ void comb_split_row(const uint16_t* __restrict__ fram
     }
   }
   __syncthreads();
-  if constexpr (D3) {
+  if constexpr (D3 && !OF) {
     // __k = |F0 - F2| + |(F1 - F2) - (F1 - F0)| (ints), fed to lp_3d for h = 13..839
     for (int h = tid; h < IN_X; h += 256) {
       double k = 0.0;
@@ -371,19 +376,27 @@ __device__ __forceinline__ void comb_split_row(const uint16_t* __restrict__ fram
     if (h >= 4 && h < 840) {
       double cavg = 0;
       if constexpr (D3) {
-        // _k[h] = lp_3d output of the feed at h + 8 (h = 5..831), the raw __k at
-        // 836..839, 0 at 4 and 832..835 (never written in the reference)
-        double kk = 0.0;
-        if (h >= 5 && h <= 831) {
+        double k2, clp2;
+        if constexpr (OF) {
+          // the flow's weight (OpticalFlow3D writes frame rows 0..503, columns 70..909)
+          k2 = (l < 2 * flow::FR && h >= flow::FX0) ? kmap[(size_t)f * flow::FR * flow::FC +
+                                                           (size_t)(l >> 1) * flow::FC + (h - flow::FX0)] : 0.0;
+          clp2 = (double)((int)s_pn[1][h] - (int)s_raw[1][h]);    // p3line (Frame[0], the next frame) - line
+        } else {
+          // _k[h] = lp_3d output of the feed at h + 8 (h = 5..831), the raw __k at
+          // 836..839, 0 at 4 and 832..835 (never written in the reference)
+          double kk = 0.0;
+          if (h >= 5 && h <= 831) {
 #pragma unroll
-          for (int t = 0; t < 17; t++) kk += (g_lp3d.b[t] / 1.0) * s_x[h + 8 - t];
-        } else if (h >= 836) {
-          kk = s_x[h];
+            for (int t = 0; t < 17; t++) kk += (g_lp3d.b[t] / 1.0) * s_x[h + 8 - t];
+          } else if (h >= 836) {
+            kk = s_x[h];
+          }
+          k2 = clampd(1 - ((kk - core) / range), 0, 1);
+          clp2 = (double)((((int)s_pn[1][h] + (int)s_pn[0][h]) / 2) - (int)s_raw[1][h]);
         }
-        const double k2 = clampd(1 - ((kk - core) / range), 0, 1);
         const double k1 = (l <= 523) ? 1 - k2 : 0.0;     // Split3D :401-403 (Split2D left line 524 at 0)
         const double k0 = 1 - k2 - k1;
-        const double clp2 = (double)((((int)s_pn[1][h] + (int)s_pn[0][h]) / 2) - (int)s_raw[1][h]);
         const double clp1 = (l < 524 && h >= 18) ? clp1_lds(s_c[0], s_c[1], s_c[2], h, P_2DRANGE, adaptive) : 0.0;
         cavg += clp2 * k2;
         cavg += clp1 * k1;
@@ -420,6 +433,12 @@ extern "C" __global__ __launch_bounds__(256) void ldg_k_comb_split3(const uint16
                                                                     double* __restrict__ cvbuf, double core,
                                                                     double range, CombOpt O) {
   comb_split_row<true>(frames, cvbuf, core, range, O);
+}
+// 3D with optical flow (-d 3): frames[n] must be valid; kmap: one weight map per frame.
+extern "C" __global__ __launch_bounds__(256) void ldg_k_comb_split3_of(const uint16_t* __restrict__ frames,
+                                                                       double* __restrict__ cvbuf, CombOpt O,
+                                                                       const double* __restrict__ kmap) {
+  comb_split_row<true, CombOpt, true>(frames, cvbuf, 0.0, 1.0, O, kmap);
 }
 
 // ---- ldg_k_comb_iq: FilterIQ's two chains of every row with line >= 44, one

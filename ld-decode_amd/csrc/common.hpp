@@ -105,6 +105,14 @@ __device__ __forceinline__ void prio_latency() { __builtin_amdgcn_s_setprio(3); 
 
 }  // namespace ldg
 
+// The optical-flow fields of the 3D comb with flow (flow.hip, comb.hip): 252 x 840
+// luma fields, rows 23 + field + 2 y and columns 70..909 of a 525 x 910 frame.
+namespace ldg {
+namespace flow {
+constexpr int FR = 252, FC = 840, FY0 = 23, FX0 = 70;
+}  // namespace flow
+}  // namespace ldg
+
 // Per-kernel phase stamps (profiling builds only, -DLDG_STAMPS; tools/kstamps.py):
 // thread 0 of the first KST_BLOCKS workgroups of kernel K records the shader
 // clock at phase boundary i (after a workgroup barrier).

@@ -69,11 +69,12 @@ class CombOpts(C.Structure):
     """ldg_comb_opts (include/ldgpu.h): comb-ntsc's command-line options."""
     _fields_ = [('black_ire', C.c_double), ('brightness', C.c_double), ('nr_y', C.c_double), ('nr_c', C.c_double),
                 ('bw', C.c_int32), ('adaptive2d', C.c_int32), ('colorlpf', C.c_int32), ('colorlpf_hq', C.c_int32),
-                ('linesout', C.c_int32), ('debug_line', C.c_int32), ('wide', C.c_int32)]
+                ('linesout', C.c_int32), ('debug_line', C.c_int32), ('wide', C.c_int32),
+                ('opticalflow', C.c_int32)]
 
 
 COMB_DEFAULTS = dict(black_ire=7.5, brightness=236.0, nr_y=1.0, nr_c=0.0, bw=False, adaptive2d=True, colorlpf=True,
-                     colorlpf_hq=True, linesout=480, debug_line=-1000, wide=False)
+                     colorlpf_hq=True, linesout=480, debug_line=-1000, wide=False, opticalflow=False)
 
 
 class Filters(C.Structure):
@@ -383,8 +384,9 @@ class Context:
         return out
 
     def comb_ntsc3d(self, frames, core_ire=-1.0, range_ire=-1.0):
-        """3D NTSC comb without optical flow (comb-ntsc -d 3 -F): n x (525, 910) uint16 frames in,
-        the rgb48 frames that now have both neighbours out (none for a process's first two frames)."""
+        """3D NTSC comb, comb-ntsc -d 3 -F (or, after comb_set_opts(opticalflow=True), -d 3 with
+        the build-defined optical flow): n x (525, 910) uint16 frames in, the rgb48 frames that
+        now have both neighbours out (none for a process's first two frames)."""
         f = np.ascontiguousarray(frames, dtype=np.uint16).reshape(-1, 525 * 910)
         out = np.zeros((f.shape[0], self.comb_lines, self.comb_width, 3), dtype=np.uint16)
         n_out = C.c_int(0)

@@ -30,6 +30,9 @@ def _load():
     lib.comb3d_process.restype = C.c_int
     lib.comb3d_aburstlev.argtypes = [C.c_void_p]
     lib.comb3d_aburstlev.restype = C.c_double
+    lib.comb2d_process_of.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
+    lib.comb2d_flow_luma.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
+    lib.comb2d_set_nr_min.argtypes = [C.c_void_p, C.c_double]
     return lib
 
 
@@ -103,6 +106,66 @@ class Comb3D:
     @property
     def aburstlev(self):
         return self.lib.comb3d_aburstlev(self.h)
+
+
+class Comb3DFlow:
+    """One reference comb process run as `comb-ntsc -d 3` (optical flow; comb-ntsc.cxx
+    Process :834-892 with f = 1, OpticalFlow3D :600-662, Split3D(f, true) :369-412).
+    BUILD-DEFINED and parity unpinned: the flow is oracle/farneback.py's restatement of
+    OpenCV's Farneback.  Per input frame g: from g = 1 the flow path's luma fields; from
+    g = 2 the flow against the previous frame's (the last flow as the initial estimate from
+    g = 3) and the weight map of frame g - 1, which is then output (clp2 = frame g -
+    frame g - 1): nothing for the first two inputs, one frame late, never the last.  The
+    flow path raises the Y / C noise-reduction clips to 4 (raw) from the second frame."""
+
+    def __init__(self, core_ire=-1.0, range_ire=-1.0, **opts):
+        self.lib = _load()
+        self.h = self.lib.comb2d_create()
+        self.opts = _set_opts(self.lib.comb2d_set_opts, self.h, opts)
+        # comb-ntsc main() with flow: p_3dcore / p_3drange 0 / 0.5 IRE by default, times irescale
+        self.core = (0.0 if core_ire < 0 else core_ire) * 358.4
+        self.range = (0.5 if range_ire < 0 else range_ire) * 358.4
+        self.g, self.prev_fields, self.flow, self.held = 0, None, None, None
+        self.kmaps = {}
+
+    def __del__(self):
+        if getattr(self, 'h', None):
+            self.lib.comb2d_destroy(self.h)
+            self.h = None
+
+    def luma_fields(self, frame):
+        from .farneback import field_images
+        y = np.zeros((IN_Y, IN_X), dtype=np.float64)
+        f = np.ascontiguousarray(frame, dtype=np.uint16)
+        self.lib.comb2d_flow_luma(self.h, f.ctypes.data, y.ctypes.data)
+        return field_images(y)
+
+    def process(self, frames):
+        from .farneback import combk_from_flow, farneback
+        f = np.ascontiguousarray(frames, dtype=np.uint16).reshape(-1, IN_Y, IN_X)
+        W = IN_X if self.opts['wide'] else OUT_W
+        outs = []
+        for fr in f:
+            g = self.g
+            self.g += 1
+            if g >= 1:
+                self.lib.comb2d_set_nr_min(self.h, 4.0)
+                cur = self.luma_fields(fr)
+                if g >= 2:
+                    init = self.flow if g >= 3 else [None, None]
+                    self.flow = [farneback(cur[k], self.prev_fields[k], init[k]) for k in range(2)]
+                    km = np.ascontiguousarray(combk_from_flow(self.flow[0], self.flow[1], self.core, self.range))
+                    out = np.zeros((self.opts['linesout'], W, 3), dtype=np.uint16)
+                    self.lib.comb2d_process_of(self.h, self.held.ctypes.data, fr.ctypes.data, km.ctypes.data,
+                                               out.ctypes.data)
+                    outs.append(out)
+                self.prev_fields = cur
+            self.held = np.ascontiguousarray(fr)
+        return np.stack(outs) if outs else np.zeros((0, self.opts['linesout'], W, 3), dtype=np.uint16)
+
+    @property
+    def aburstlev(self):
+        return self.lib.comb2d_aburstlev(self.h)
 
 
 PAL_IN_X, PAL_IN_Y, PAL_OUT_W, PAL_OUT_H = 1135, 625, 1057, 576

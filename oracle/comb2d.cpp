@@ -80,6 +80,7 @@ const double NRC_B[17] = {
 struct Opts {
   double black_ire = 7.5, brightness = 236, nr_y = 1.0, nr_c = 0.0;
   int bw = 0, adaptive2d = 1, colorlpf = 1, colorlpf_hq = 1, linesout = 480, debugline = -1000, wide = 0;
+  double nr_min = 0;   // raw: the 3D flow path's DoYNR / DoCNR(..., 4) raise both clips to 4 (:487-488,527-529)
   int out_w() const { return wide ? IN_X : OUT_W; }
   int out_x0() const { return wide ? 0 : OUT_X0; }
 };
@@ -117,13 +118,17 @@ struct Comb {
   Fir<25> hpy{NR_B};
   Fir<17> hpi{NRC_B}, hpq{NRC_B};
   int firstline() const { return (o.linesout == IN_Y) ? 20 : 38; }
-  double nr_y() const { return o.nr_y * IRESCALE; }   // main(): nr_y *= irescale
-  double nr_c() const { return o.nr_c * IRESCALE; }
+  double nr_y() const { return std::max(o.nr_y * IRESCALE, o.nr_min); }   // main(): nr_y *= irescale
+  double nr_c() const { return std::max(o.nr_c * IRESCALE, o.nr_min); }
 
   // prev / next: the frames before and after `raw` for the 3D path (-d 3 -F),
-  // null for 2D; core / range: p_3dcore / p_3drange (already times irescale)
+  // null for 2D; core / range: p_3dcore / p_3drange (already times irescale).
+  // kmap (3D with optical flow, Split3D(f, true) :395-407): combk[2] per pixel (525 x 910,
+  // from the flow of OpticalFlow3D, oracle/farneback.py), clp2 = next - raw; prev unused.
+  // luma_out: instead of colour, the flow path's luma (AdjustY + DoYNR of the 2D
+  // decode, comb-ntsc.cxx:851-856) as 525 x 910 doubles (rgb unused).
   void process(const uint16_t* raw, uint16_t* rgb, const uint16_t* prev = nullptr, const uint16_t* next = nullptr,
-               double core = 0, double range = 1) {
+               double core = 0, double range = 1, const double* kmap = nullptr, double* luma_out = nullptr) {
     // ---- Split1D: clp0 (lines 44..524), combk0 = 1 there
     static double clp0[IN_Y + 2][IN_X], clp1[IN_Y][IN_X], k0[IN_Y][IN_X], k1[IN_Y][IN_X];
     std::memset(clp0, 0, sizeof(clp0));
@@ -183,7 +188,17 @@ struct Comb {
     static double clp2[IN_Y][IN_X], k2[IN_Y][IN_X];
     std::memset(clp2, 0, sizeof(clp2));
     std::memset(k2, 0, sizeof(k2));
-    if (prev) {
+    if (kmap) {
+      for (int l = 36; l < IN_Y; l++) {
+        for (int h = 4; h < 840; h++) {
+          const int adr = l * IN_X + h;
+          clp2[l][h] = (double)((int)next[adr] - (int)raw[adr]);
+          k2[l][h] = kmap[adr];
+          if (l >= 2 && l <= 523) k1[l][h] = 1 - k2[l][h];
+          k0[l][h] = 1 - k2[l][h] - k1[l][h];
+        }
+      }
+    } else if (prev) {
       for (int l = 36; l < IN_Y; l++) {
         const int o = l * IN_X;
         double x[IN_X] = {0}, kk[IN_X] = {0};   // __k fed at h = 13..839; _k[4], _k[832..835] stay 0
@@ -251,6 +266,24 @@ struct Comb {
         y.y += comp;
         cb[l][h] = y;
       }
+    }
+    if (luma_out) {
+      // the flow path: AdjustY above, then DoYNR with its taps inside the row (h >= 70 is
+      // all the flow reads), no FilterIQ / VBI copy; rows below firstline keep SplitIQ's Y
+      const double NRY = nr_y();
+      for (int l = 0; l < IN_Y; l++)
+        for (int h = 0; h < IN_X; h++) {
+          double y = cb[l][h].y;
+          if (l >= FL && NRY > 0 && h >= 40 && h + 12 <= 843) {
+            double y0 = 0;
+            for (int q = 0; q < 25; q++) y0 += (NR_B[q] / 1.0) * cb[l][h + 12 - q].y;
+            double a = y0;
+            if (std::fabs(a) > NRY) a = (a > 0) ? NRY : -NRY;
+            y = cb[l][h].y - a;
+          }
+          luma_out[l * IN_X + h] = y;
+        }
+      return;
     }
     // ---- FilterIQ (lines 44..524, f_colorlpf): fresh colorlpi for I and for Q (colorlpq
     //      without HQ) per line, output 2 px back
@@ -365,6 +398,17 @@ void comb2d_process(void* c, int n, const uint16_t* frames, uint16_t* rgb) {
     cb->process(frames + (size_t)f * IN_X * IN_Y, rgb + (size_t)f * cb->o.out_w() * cb->o.linesout * 3);
 }
 double comb2d_aburstlev(void* c) { return static_cast<Comb*>(c)->aburstlev; }
+// the 3D comb with optical flow, one output frame: raw (the frame) with next and its
+// weight map (525 x 910 doubles); state (aburstlev, FIR histories) as any frame
+void comb2d_process_of(void* c, const uint16_t* raw, const uint16_t* next, const double* kmap, uint16_t* rgb) {
+  static_cast<Comb*>(c)->process(raw, rgb, raw, next, 0, 1, kmap);
+}
+// the flow path's luma of a frame (525 x 910 doubles; no state touched)
+void comb2d_flow_luma(void* c, const uint16_t* raw, double* luma) {
+  Comb tmp = *static_cast<Comb*>(c);
+  tmp.process(raw, nullptr, nullptr, nullptr, 0, 1, nullptr, luma);
+}
+void comb2d_set_nr_min(void* c, double v) { static_cast<Comb*>(c)->o.nr_min = v; }
 
 // One reference process in -d 3 -F mode: its own Comb state plus the last two
 // input frames.  Feeds n frames and writes one rgb48 frame per frame that now

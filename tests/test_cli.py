@@ -320,10 +320,28 @@ def test_cli_sharded_rccl_halo_equal_single(tmp_path):
 COMB_CLI = os.path.join(ROOT, 'ld-decode_amd', 'comb_ntsc.py')
 
 
-def test_comb_cli_rejects_optical_flow_3d():
-    r = subprocess.run([sys.executable, COMB_CLI, '-d', '3'], capture_output=True, text=True, timeout=120,
+def test_comb_cli_rejects_wide_with_optical_flow():
+    r = subprocess.run([sys.executable, COMB_CLI, '-d', '3', '-W'], capture_output=True, text=True, timeout=120,
                        stdin=subprocess.DEVNULL)
-    assert r.returncode == 1 and 'use -d 3 -F' in r.stderr
+    assert r.returncode == 1 and 'use -d 3 -F -W' in r.stderr
+
+
+@pytest.mark.gpu
+def test_comb_cli_3d_optical_flow_encode_script_form(tmp_path):
+    """`comb -d 3 -I 0` as encode-ntsc:4 / encode-ralf:6 run it (3D with optical flow, the
+    reference's default): the stream filter against the oracle's restatement (build-defined
+    Farneback, oracle/farneback.py) within +-1 LSB, chunked across calls."""
+    sys.path.insert(0, HERE)
+    from test_comb import frames_3d
+    from oracle.comb import Comb3DFlow
+    fr = frames_3d(seed=5, n=5)
+    r = subprocess.run([sys.executable, COMB_CLI, '--chunk', '2', '-d', '3', '-I', '0'], input=fr.tobytes(),
+                       capture_output=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-2000:]
+    exp = Comb3DFlow(black_ire=0.0).process(fr)
+    got = np.frombuffer(r.stdout, dtype=np.uint16).reshape(-1, 480, 744, 3)
+    assert got.shape == exp.shape == (3, 480, 744, 3)
+    assert np.abs(got.astype(np.int64) - exp.astype(np.int64)).max() <= 1
 
 
 @pytest.mark.gpu
