@@ -48,8 +48,11 @@ def parse(argv=None):
     p.add_argument('--comb-3d', action='store_true',
                    help='with --comb: the 3D comb without optical flow (comb-ntsc -d 3 -F); '
                         'every frame but the first and the last')
-    p.add_argument('--comb-3d-core', type=float, default=-1.0, help='comb-ntsc -c (IRE, default 1.25)')
-    p.add_argument('--comb-3d-range', type=float, default=-1.0, help='comb-ntsc -r (IRE, default 5.5)')
+    p.add_argument('--comb-3d-flow', action='store_true',
+                   help='with --comb: the 3D comb with optical flow (comb-ntsc -d 3; the flow is this build\'s '
+                        'restatement of OpenCV\'s Farneback, build-defined); every frame but the first and the last')
+    p.add_argument('--comb-3d-core', type=float, default=-1.0, help='comb-ntsc -c (IRE, default 1.25; 0 with flow)')
+    p.add_argument('--comb-3d-range', type=float, default=-1.0, help='comb-ntsc -r (IRE, default 5.5; 0.5 with flow)')
     p.add_argument('--comb-args', default='',
                    help="comb-ntsc options for --comb (NTSC), e.g. '-I 0 -N 1 -v' (comb_ntsc.py's -I -b -n -N "
                         "-B -a -L -Q -v -l -W)")
@@ -72,6 +75,8 @@ def main(argv=None):
         print("ERROR: Can only be PAL or NTSC")
         return 1
     system = 'PAL' if args.pal else 'NTSC'
+    if args.comb_3d_flow:
+        args.comb_3d = True
     if args.comb and system != 'NTSC' and args.comb_3d:
         print("ERROR: --comb-3d is NTSC only")
         return 1
@@ -104,7 +109,11 @@ def main(argv=None):
                 system != 'NTSC':
             print("ERROR: --comb-args takes comb-ntsc's arithmetic options (-I -b -n -N -B -a -L -Q -v -l), NTSC")
             return 1
+        if args.comb_3d_flow:
+            ca.opts['opticalflow'] = True
         dec.ctx.comb_set_opts(**ca.opts)
+    elif args.comb_3d_flow:
+        dec.ctx.comb_set_opts(opticalflow=True)
     samples_per_frame = dec.rf.samples_per_frame                 # int(fs / FPS) + 1
     bytes_per_frame = samples_per_frame * 5 // 4                 # for 10-bit packed files
     infile_size = os.path.getsize(filename)

@@ -378,6 +378,22 @@ def test_cli_comb_3d(tmp_path):
 
 
 @pytest.mark.gpu
+def test_cli_comb_3d_flow(tmp_path):
+    """lddecode.py --comb --comb-3d-flow: the decoded frames through the 3D comb with optical
+    flow (build-defined, oracle/comb.py Comb3DFlow), +-1 LSB."""
+    cap, gold = _golden_capture(tmp_path)
+    out = tmp_path / 'out'
+    r = run_cli('--comb', '--comb-3d-flow', cap, out)
+    assert r.returncode == 0, r.stderr[-2000:]
+    frames = np.fromfile(str(out) + '.tbc', dtype=np.uint16).reshape(-1, 525, 910)
+    rgb = np.fromfile(str(out) + '.rgb', dtype=np.uint16).reshape(-1, 480, 744, 3)
+    assert len(rgb) == len(frames) - 2 >= 1
+    from oracle.comb import Comb3DFlow
+    o = Comb3DFlow().process(frames)
+    assert np.abs(o.astype(np.int64) - rgb.astype(np.int64)).max() <= 1
+
+
+@pytest.mark.gpu
 def test_cli_pal_comb(tmp_path):
     """lddecode.py -p --comb: PAL .tbc through the build-defined PAL Y/C decoder, against
     its oracle on the same frames (+-1 LSB)."""
