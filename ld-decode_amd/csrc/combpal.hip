@@ -9,11 +9,11 @@
 //   ldg_k_pal_split  one workgroup per (frame, line 24..624): raw lines l-4,
 //                    l, l+4 -> Split1D (+-2 px) / Split2D (+-4 lines) ->
 //                    SplitIQ's signed chroma cv[h] (the held U / V source);
-//   ldg_k_pal_angle  one workgroup for all frames of the call, in order: each
-//                    line's burst angle (sum of the held U / V over the burst
-//                    window, after AdjustY's 2-px shift on lines >= 44), the
-//                    frame's V-switch phase vote, and the sequential
-//                    burst-level EMA (constant level 8 in the reference);
+//   ldg_k_pal_angle  one workgroup per frame: each line's burst angle (sum of
+//                    the held U / V over the burst window, after AdjustY's
+//                    2-px shift on lines >= 44), the frame's V-switch phase
+//                    vote, and the burst-level EMA (constant level 8 in the
+//                    reference: a chain that sits at its fixed point);
 //   ldg_k_pal_out    one workgroup per (frame, output row): AdjustY, Y-NR
 //                    (taps within the line for x >= 78), rotation of U / V
 //                    to a 135-degree burst, the V-switch flip, YUV -> RGB.
@@ -101,57 +101,81 @@ extern "C" __global__ __launch_bounds__(256) void ldg_k_pal_split(const uint16_t
   }
 }
 
-// grid: 1 workgroup of 256 threads.  angle: [n][IN_Y] degrees; phase: [n];
-// abl: [n][ABL_LINES] (the EMA value line 44 + j uses); state[0]: the EMA
-// carried across calls (-1 = not initialised).
+// grid: n workgroups of 256 threads, one per frame.  angle: [n][IN_Y] degrees;
+// phase: [n]; abl: [n][ABL_LINES] (the EMA value line 44 + j uses).  The EMA is
+// carried across calls: it enters from state_in[0] (-1 = not initialised) and
+// the last frame's workgroup leaves it in state_out[0] (a different double: the
+// other workgroups read state_in meanwhile).  Its input is the constant burst
+// level 8, so the chain reaches a fixed point (ema(a) == a, at once from "not
+// initialised": 8 * .99 + 8 * .01 == 8) and every workgroup runs it from
+// state_in only until then, exactly as the sequential chain would.
 extern "C" __global__ __launch_bounds__(256) void ldg_k_pal_angle(const double* __restrict__ cvbuf, int n,
                                                                   double* __restrict__ angle,
                                                                   int32_t* __restrict__ phase,
-                                                                  double* __restrict__ state,
+                                                                  const double* __restrict__ state_in,
+                                                                  double* __restrict__ state_out,
                                                                   double* __restrict__ abl) {
   prio_latency();
   __shared__ double s_ang[pal::IN_Y];
-  __shared__ int s_cnt;
+  __shared__ int s_cnt, s_fix;
+  __shared__ double s_a;
   const int tid = threadIdx.x;
-  double a = state[0];
-  for (int f = 0; f < n; f++) {
-    for (int l = tid; l < pal::IN_Y; l += 256) {
-      double i = 0, q = 0;
-      if (l >= pal::SPLIT_L0) {
-        const double* cv = cvbuf + ((size_t)f * pal::CV_ROWS + (l - pal::SPLIT_L0)) * pal::CV_STRIDE;
-        const int sh = (l >= pal::FIRST_LINE) ? 2 : 0;    // AdjustY's p[h] = p[h + 2]
-        for (int h = pal::BURST_H0; h < pal::BURST_H1; h++) {
-          i += pal::held_i(cv, h + sh);
-          q += pal::held_q(cv, h + sh);
-        }
-      }
-      double rv = 0.0;
-      if (l >= 10) {
-        rv = atan2(q, i) * (180 / 3.141592653589793);
-        if (rv < 0) rv += 360;
-      }
-      s_ang[l] = rv;
-      angle[(size_t)f * pal::IN_Y + l] = rv;
-    }
-    if (tid == 0) s_cnt = 0;
-    __syncthreads();
-    int c = 0;
-    for (int l = 20 + 4 * tid; l < pal::IN_Y - 4; l += 4 * 256) c += fabs(s_ang[l + 1] - s_ang[l]) < 20;
-    if (c) atomicAdd(&s_cnt, c);
-    __syncthreads();
-    if (tid == 0) {
-      const int tot = (pal::IN_Y - 4 - 20 + 3) / 4;
-      phase[f] = s_cnt > (tot / 2) ? 1 : 0;
-      for (int j = 0; j < pal::ABL_LINES; j++) {   // burstlev = 8 (> 5) on every line
-        const double bl = 8;
-        if (a < 0) a = bl;
-        a = (a * .99) + (bl * .01);
-        abl[(size_t)f * pal::ABL_LINES + j] = a;
+  const int f = blockIdx.x;
+  for (int l = tid; l < pal::IN_Y; l += 256) {
+    double i = 0, q = 0;
+    if (l >= pal::SPLIT_L0) {
+      const double* cv = cvbuf + ((size_t)f * pal::CV_ROWS + (l - pal::SPLIT_L0)) * pal::CV_STRIDE;
+      const int sh = (l >= pal::FIRST_LINE) ? 2 : 0;    // AdjustY's p[h] = p[h + 2]
+      for (int h = pal::BURST_H0; h < pal::BURST_H1; h++) {
+        i += pal::held_i(cv, h + sh);
+        q += pal::held_q(cv, h + sh);
       }
     }
-    __syncthreads();
+    double rv = 0.0;
+    if (l >= 10) {
+      rv = atan2(q, i) * (180 / 3.141592653589793);
+      if (rv < 0) rv += 360;
+    }
+    s_ang[l] = rv;
+    angle[(size_t)f * pal::IN_Y + l] = rv;
   }
-  if (tid == 0) state[0] = a;
+  if (tid == 0) {
+    s_cnt = 0;
+    // burstlev = 8 (> 5) on every line: a -> (a < 0 ? 8 : a) * .99 + 8 * .01
+    const double bl = 8;
+    double a = state_in[0];
+    const int64_t skip = (int64_t)f * pal::ABL_LINES;   // the EMA steps of the earlier frames
+    for (int64_t j = 0; j < skip; j++) {
+      const double an = ((a < 0) ? bl : a) * .99 + bl * .01;
+      if (an == a) break;
+      a = an;
+    }
+    double* out = abl + (size_t)f * pal::ABL_LINES;
+    int j = 0;
+    for (; j < pal::ABL_LINES; j++) {
+      const double an = ((a < 0) ? bl : a) * .99 + bl * .01;
+      if (an == a) break;
+      a = an;
+      out[j] = a;
+    }
+    s_fix = j;
+    s_a = a;
+    if (f == n - 1) state_out[0] = a;
+  }
+  __syncthreads();
+  {
+    double* out = abl + (size_t)f * pal::ABL_LINES;
+    const double a = s_a;
+    for (int j = s_fix + tid; j < pal::ABL_LINES; j += 256) out[j] = a;
+  }
+  int c = 0;
+  for (int l = 20 + 4 * tid; l < pal::IN_Y - 4; l += 4 * 256) c += fabs(s_ang[l + 1] - s_ang[l]) < 20;
+  if (c) atomicAdd(&s_cnt, c);
+  __syncthreads();
+  if (tid == 0) {
+    const int tot = (pal::IN_Y - 4 - 20 + 3) / 4;
+    phase[f] = s_cnt > (tot / 2) ? 1 : 0;
+  }
 }
 
 // grid: n * OUT_H workgroups of 256 threads.

@@ -793,8 +793,12 @@ __device__ __forceinline__ double* pilot_base(double* scratch, int slot) {
 }  // namespace
 
 // grid: n_reads * MAX_LINES workgroups of 64 threads (one wave per line): the
-// wave forms the flipped (demod - demod_05) of the window in LDS; lane 0 walks
-// the crossings as the reference does.
+// wave forms the flipped (demod - demod_05) of the window in LDS.  The
+// reference's crossing walk (i -> int(zc + 1) + 1 after a crossing, i + 1
+// otherwise) only ever starts calczc at qualifying positions, and calczc's
+// result does not depend on the walk: every lane evaluates its own positions
+// first, then the walk is a bit scan over the qualifying mask (one LDS read per
+// crossing).  The per-line median of offsets[1:-1] is a rank sort across lanes.
 extern "C" __global__ __launch_bounds__(64) void ldg_k_pilot_lines(const int32_t* __restrict__ smap,
                                                                    const double* __restrict__ video,
                                                                    int64_t vread_stride, int64_t vchan_stride,
@@ -803,8 +807,11 @@ extern "C" __global__ __launch_bounds__(64) void ldg_k_pilot_lines(const int32_t
                                                                    double* __restrict__ scratch) {
   prio_latency();
 
-  constexpr int PW = 256;
+  constexpr int PW = 256;                       // 4.7 us at 40 MSPS: 188 samples
   __shared__ double s_pil[PW];
+  __shared__ double s_zc[PW];
+  __shared__ double s_off[PILOT_MAX];
+  __shared__ double s_srt[PILOT_MAX];
   const int lane = threadIdx.x;
   const int slot = smap[blockIdx.x / MAX_LINES];
   const int l = blockIdx.x % MAX_LINES;
@@ -821,87 +828,185 @@ extern "C" __global__ __launch_bounds__(64) void ldg_k_pilot_lines(const int32_t
   int64_t a, b;
   py_slice(py_int(ll[l] - 4.7 * C.freq), py_int(ll[l]), len, a, b);
   const int pn = (int)(b > a ? b - a : 0);
-  const int pm = pn < PW ? pn : PW;
-  if (pm > 0) {
-    const double* d05 = video + (int64_t)slot * vread_stride + (int64_t)CH_05 * vchan_stride;
-    for (int q = lane; q < pm; q += 64) s_pil[q] = dm[b - 1 - q] - d05[b - 1 - q];   // np.flip
-    __syncthreads();
+  const int pm = pn < PW ? pn : PW;             // pn <= PW at the reference's sample rates
+  const double* d05 = video + (int64_t)slot * vread_stride + (int64_t)CH_05 * vchan_stride;
+  for (int q = lane; q < pm; q += 64) s_pil[q] = dm[b - 1 - q] - d05[b - 1 - q];   // np.flip
+  __syncthreads();
+  uint64_t qm[PW / 64];
+#pragma unroll
+  for (int j = 0; j < PW / 64; j++) {
+    const int i = lane + 64 * j;
+    bool q = false;
+    if (i < pm && inrange(s_pil[i], -300000, -100000)) {
+      double zc;
+      if (calczc(s_pil, pm, (double)i, 0.0, 10, &zc) == 0) {
+        s_zc[i] = zc;
+        q = true;
+      }
+    }
+    qm[j] = __ballot(q);
   }
-  if (lane != 0) return;
-  const double* pil = s_pil;
+  __syncthreads();
   double adjfreq = C.freq;
   if (l > 1) adjfreq /= (ll[l] - ll[l - 1]) / (double)C.linelen;
   int cnt = 0, i = 0;
-  while (i < pn) {
-    if (inrange(pil[i], -300000, -100000)) {
-      double zc;
-      if (calczc(pil, pm, (double)i, 0.0, 10, &zc) == 0) {
-        const double zcp = zc / (adjfreq / 3.75);
-        if (cnt < PILOT_MAX) offs[cnt] = zcp - floor(zcp);
-        cnt++;
-        i = (int)(zc + 1);
-      }
+  double myoff = 0.0;                           // offsets[l][lane]
+  while (i < pm) {
+    int nxt = -1;
+#pragma unroll
+    for (int j = 0; j < PW / 64; j++) {
+      uint64_t m = qm[j];
+      if ((i >> 6) > j) m = 0;
+      else if ((i >> 6) == j) m &= ~0ull << (i & 63);
+      if (nxt < 0 && m) nxt = 64 * j + __ffsll((unsigned long long)m) - 1;
     }
-    i += 1;
+    if (nxt < 0) break;
+    const double zc = s_zc[nxt];
+    const double zcp = zc / (adjfreq / 3.75);
+    if (lane == cnt) myoff = zcp - floor(zcp);
+    cnt++;
+    i = (int)(zc + 1) + 1;
   }
+  if (i < pn) i = pn;                           // the walk runs on to the window's end
   if (cnt > PILOT_MAX) cnt = PILOT_MAX;
   // offsets[l][1:-1] for l >= 2 (len(offsets dict) >= 3); kept in alloffsets if i >= 11
-  int keep = 0;
+  int keep = 0, k = 0;
   double med = 0.0;
   if (l >= 2) {
-    const int k = cnt >= 2 ? cnt - 2 : 0;
-    for (int q = 0; q < k; q++) offs[q] = offs[q + 1];
-    cnt = k;
+    k = cnt >= 2 ? cnt - 2 : 0;
     keep = (i >= 11) ? 1 : 0;
-    if (cnt > 0) {
-      double tmp[PILOT_MAX];
-      med = np_median(offs, cnt, tmp);
+    const bool mine = lane >= 1 && lane <= k;
+    if (mine) {
+      s_off[lane - 1] = myoff;
+      offs[lane - 1] = myoff;
     }
-  } else {
-    cnt = 0;
+    __syncthreads();
+    if (mine) {                                 // stable rank = np.sort position
+      int r = 0;
+      for (int t = 0; t < k; t++) {
+        const double v = s_off[t];
+        r += (v < myoff) || (v == myoff && t < lane - 1);
+      }
+      s_srt[r] = myoff;
+    }
+    __syncthreads();
+    if (k > 0) med = sorted_median(s_srt, k);
   }
-  meta[3 * l + 0] = cnt;
-  meta[3 * l + 1] = keep;
-  meta[3 * l + 2] = med;
+  if (lane == 0) {
+    meta[3 * l + 0] = k;
+    meta[3 * l + 1] = keep;
+    meta[3 * l + 2] = med;
+  }
 }
 
+namespace {
+// k-th smallest dkey of a[0..n) (0 <= k < n, no NaNs), whole 256-thread block:
+// radix select, 8 bits per pass, the digit chosen by wave 0.
+__device__ uint64_t block_kth_key(const double* a, int n, int k, int tid, int* hist, int* sel, uint64_t* key) {
+  const int lane = tid & 63;
+  uint64_t prefix = 0, mask = 0;
+  for (int shift = 56; shift >= 0; shift -= 8) {
+    hist[tid] = 0;
+    __syncthreads();
+    for (int i = tid; i < n; i += 256) {
+      const uint64_t u = dkey(a[i]);
+      if ((u & mask) == prefix) atomicAdd(&hist[(u >> shift) & 255], 1);
+    }
+    __syncthreads();
+    if (tid < 64) {
+      int c[4], tot = 0;
+#pragma unroll
+      for (int e = 0; e < 4; e++) { c[e] = hist[4 * lane + e]; tot += c[e]; }
+      int incl = tot;
+      for (int o = 1; o < 64; o <<= 1) {
+        const int v = __shfl_up(incl, o);
+        if (lane >= o) incl += v;
+      }
+      const int excl = incl - tot;
+      if (k >= excl && k < incl) {
+        int run = excl, digit = -1;
+#pragma unroll
+        for (int e = 0; e < 4; e++) {
+          if (digit < 0 && k < run + c[e]) { digit = 4 * lane + e; sel[0] = digit; sel[1] = run; sel[2] = c[e]; }
+          run += c[e];
+        }
+      }
+    }
+    __syncthreads();
+    const int digit = sel[0], below = sel[1], cnt = sel[2];
+    k -= below;
+    prefix |= (uint64_t)digit << shift;
+    mask |= (uint64_t)255 << shift;
+    if (cnt == 1 && shift > 0) {
+      // one key left with this prefix: it is the k-th
+      for (int i = tid; i < n; i += 256) {
+        const uint64_t u = dkey(a[i]);
+        if ((u & mask) == prefix) *key = u;
+      }
+      __syncthreads();
+      const uint64_t r = *key;
+      __syncthreads();
+      return r;
+    }
+    __syncthreads();
+  }
+  return prefix;
+}
+}  // namespace
+
+// grid: n reads x 256 threads.  alloffsets (the kept lines' offsets, line order)
+// gathered by a block scan of the per-line counts, np.median by radix select,
+// then every line's adjustment in parallel.
 extern "C" __global__ __launch_bounds__(256) void ldg_k_pilot_field(const int32_t* __restrict__ smap,
                                                                     FieldRec* __restrict__ recs,
                                                                     double* __restrict__ lines, SysConst C,
                                                                     double* __restrict__ scratch) {
   prio_latency();
 
-  __shared__ double s_all[8192];
-  __shared__ int s_n;
-  const int tid = threadIdx.x;
+  constexpr int NALL = 8192;
+  static_assert(MAX_LINES <= 512, "two lines per thread");
+  __shared__ double s_all[NALL];
+  __shared__ int s_wsum[4];
+  __shared__ int s_hist[256];
+  __shared__ int s_sel[3];
+  __shared__ uint64_t s_key;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int slot = smap[blockIdx.x];
   FieldRec* R = recs + slot;
   if (R->status != FS_PENDING) return;
   const int nl = R->nlines;
   double* P = pilot_base(scratch, slot);
   const double* meta = P + (int64_t)MAX_LINES * PILOT_MAX;
-  if (tid == 0) {
-    int n = 0;
-    for (int l = 0; l < nl; l++) {
-      if (!meta[3 * l + 1]) continue;
-      const int c = (int)meta[3 * l + 0];
-      for (int q = 0; q < c && n < 8192; q++) s_all[n++] = P[(int64_t)l * PILOT_MAX + q];
-    }
-    s_n = n;
+  const int l0 = 2 * tid, l1 = 2 * tid + 1;
+  const int c0 = (l0 < nl && meta[3 * l0 + 1] != 0) ? (int)meta[3 * l0 + 0] : 0;
+  const int c1 = (l1 < nl && meta[3 * l1 + 1] != 0) ? (int)meta[3 * l1 + 0] : 0;
+  const int tot = c0 + c1;
+  int incl = tot;
+  for (int o = 1; o < 64; o <<= 1) {
+    const int v = __shfl_up(incl, o);
+    if (lane >= o) incl += v;
   }
+  if (lane == 63) s_wsum[w] = incl;
   __syncthreads();
-  const int n = s_n;
-  int np2 = 1;
-  while (np2 < n) np2 <<= 1;
-  for (int k = n + tid; k < np2; k += 256) s_all[k] = __builtin_inf();
+  int off = incl - tot;
+  for (int q = 0; q < w; q++) off += s_wsum[q];
+  const int total = s_wsum[0] + s_wsum[1] + s_wsum[2] + s_wsum[3];
+  for (int q = 0; q < c0; q++)
+    if (off + q < NALL) s_all[off + q] = P[(int64_t)l0 * PILOT_MAX + q];
+  off += c0;
+  for (int q = 0; q < c1; q++)
+    if (off + q < NALL) s_all[off + q] = P[(int64_t)l1 * PILOT_MAX + q];
   __syncthreads();
-  if (n > 1) block_bitonic_sort(s_all, np2, tid, 256);
-  if (tid != 0) return;
-  const double med = sorted_median(s_all, n);
+  const int n = total < NALL ? total : NALL;
+  double med = __builtin_nan("");               // np.median([]) is nan
+  if (n > 0) {
+    med = dkey_val(block_kth_key(s_all, n, (n - 1) / 2, tid, s_hist, s_sel, &s_key));
+    if (!(n & 1)) med = (med + dkey_val(block_kth_key(s_all, n, n / 2, tid, s_hist, s_sel, &s_key))) / 2.0;
+  }
   const double tgt = inrange(med, 0.25, 0.75) ? .5 : 0;
   const double* ll = lines + (int64_t)slot * LINES_STRIDE + LL2 * MAX_LINES;
   double* lf = lines + (int64_t)slot * LINES_STRIDE + LLF * MAX_LINES;
-  for (int l = 0; l < nl; l++) {
+  for (int l = tid; l < nl; l += 256) {
     double v = ll[l];
     if (meta[3 * l + 0] > 0) v += (tgt - meta[3 * l + 2]) * (C.freq / 3.75) * .25;
     lf[l] = v;
