@@ -1,6 +1,9 @@
 """Which reads does the planner decode without the replay using them (PAL CLV)?
 
-    python tools/pal_waste.py [--seconds 4]
+    python tools/pal_waste.py [--seconds 4] [--dump out.json]
+
+--dump writes the used read starts, the launches and every decoded read's next
+start (start + nextfieldoffset) for offline study of the read chain.
 """
 import os
 import sys
@@ -51,6 +54,13 @@ def main():
             d = min(abs(k[0] - u[0]) for u in us)
             near.append((k[0], d))
         print('launch %2d: %3d reads, %3d unused (%3d past the last used read) e.g. %s' % (i, len(b), len(un), past, near))
+    if '--dump' in sys.argv:
+        import json
+        out = {'used': seq, 'launches': [[k[0] for k in b] for b in launched],
+               'next': {str(k): int(v[0]) for k, v in dec.hints.items()},
+               'status': {str(k[0]): int(v[1].status) for k, v in dec.cache.items()}}
+        with open(sys.argv[sys.argv.index('--dump') + 1], 'w') as f:
+            json.dump(out, f)
 
 
 if __name__ == '__main__':
