@@ -506,7 +506,8 @@ def main():
     units_iso = iso_reads * samples_per_read
     achieved = bps * units_iso / (iso_ms * 1e-3) / 1e9
     traffic, lds = None, None
-    pmc = os.path.join(ROOT, 'profiles', 'pmc_traffic.json')
+    # the committed --pmc passes of this system's bench command (PAL stores the pilot channel too)
+    pmc = os.path.join(ROOT, 'profiles', 'pmc_traffic_pal.json' if pal else 'pmc_traffic.json')
     if os.path.exists(pmc):
         try:
             pj = json.load(open(pmc))
@@ -537,7 +538,7 @@ def main():
         'units_per_launch': round(units_iso), 'samples_per_read': round(samples_per_read),
         'algorithmic_bytes_per_sample': round(bps, 4),
         'algorithmic_bytes_per_launch': round(bps * units_iso),
-        'traffic_unit': 'bytes per launch, 2*FETCH_SIZE + WRITE_SIZE (profiles/pmc_traffic.json, demod_iso)',
+        'traffic_unit': 'bytes per launch, 2*FETCH_SIZE + WRITE_SIZE (profiles/%s, demod_iso)' % os.path.basename(pmc),
         'traffic_x_algorithmic': (traffic / (bps * units_iso)) if traffic else None,
         'issue': lds, 'fp64': fp64,
         'pipeline': {'launches': dom_launches, 'span_ms': round(span_ms, 4), 'hip_event_ms': round(event_ms, 4),
