@@ -411,6 +411,7 @@ def main():
     rank = int(os.environ.get('RANK', '0'))
     local = int(os.environ.get('LOCAL_RANK', '0'))
     dist = None
+    shared_device = False
     if world > 1:
         import torch
         import torch.distributed as tdist
@@ -418,6 +419,7 @@ def main():
         # one rank per GPU over RCCL; more ranks than GPUs (a rehearsal on a smaller
         # box) share devices and exchange the timing scalars over gloo
         use_nccl = ndev >= world
+        shared_device = not use_nccl
         local = local % max(ndev, 1)
         torch.cuda.set_device(local)
         tdist.init_process_group('nccl' if use_nccl else 'gloo')
@@ -467,7 +469,16 @@ def main():
     # the roofline leg: the demod alone (kernel ldg_k_demod_iso) over one full-width launch's
     # reads, ISO_ITERS launches back to back, HIP events on its stream -- the per-dispatch
     # figure a kernel trace of this command reports for ldg_k_demod_iso (profiles/)
-    iso_reads, iso_ms = dec.demod_isolated(ISO_ITERS)
+    if dist is not None and shared_device:
+        # ranks sharing a GPU (a rehearsal on a smaller box) take the leg in turn, so each
+        # times the kernel alone on the device as a one-rank-per-GPU run does
+        for r in range(world):
+            barrier()
+            if r == rank:
+                iso_reads, iso_ms = dec.demod_isolated(ISO_ITERS)
+        barrier()
+    else:
+        iso_reads, iso_ms = dec.demod_isolated(ISO_ITERS)
     reads_timed = dec.stats['reads'] - reads0
     used_timed = dec.stats['reads_used'] - used0
     checks = wl.checks()
