@@ -16,7 +16,7 @@
 //                    reference: a chain that sits at its fixed point);
 //   ldg_k_pal_out    one workgroup per (frame, output row): AdjustY, Y-NR
 //                    (taps within the line for x >= 78), rotation of U / V
-//                    to a 135-degree burst, the V-switch flip, YUV -> RGB.
+//                    to a 135-degree burst (one sincos per row), the V-switch flip, YUV -> RGB.
 #include <hip/hip_runtime.h>
 #include "common.hpp"
 
@@ -218,6 +218,8 @@ extern "C" __global__ __launch_bounds__(256) void ldg_k_pal_out(const uint16_t* 
   __syncthreads();
   const double aburst = abl[(size_t)f * pal::ABL_LINES + (l - pal::FIRST_LINE)];
   const double angleadj = 135 - angle[(size_t)f * pal::IN_Y + l];
+  double sa, ca;
+  sincos(((angleadj + 0) / 180.0) * 3.141592653589793, &sa, &ca);
   const bool ph = phase[f] != 0;
   const double m = pal::BRIGHTNESS * 255 / 100;
   uint16_t* out = rgb + ((size_t)f * pal::OUT_H + row) * pal::OUT_W * 3;
@@ -232,11 +234,11 @@ extern "C" __global__ __launch_bounds__(256) void ldg_k_pal_out(const uint16_t* 
       if (fabs(a) > pal::NR_Y) a = (a > 0) ? pal::NR_Y : -pal::NR_Y;
       yv -= a;
     }
-    double iv = pal::held_i(cv, h + 2), qv = pal::held_q(cv, h + 2);
-    const double mag = sqrt((iv * iv) + (qv * qv));
-    const double ang = atan2(qv, iv) + (((angleadj + 0) / 180.0) * 3.141592653589793);
-    iv = cos(ang) * mag;
-    qv = sin(ang) * mag;
+    // the reference's polar form, mag * cis(atan2(q, i) + adj), as a rotation by the
+    // row's angle (the same vector; rounding within the checker's +-1 LSB)
+    const double i1 = pal::held_i(cv, h + 2), q1 = pal::held_q(cv, h + 2);
+    double iv = i1 * ca - q1 * sa;
+    double qv = i1 * sa + q1 * ca;
     iv *= (10 / aburst);
     qv *= (10 / aburst);
     const double i0 = iv, q0 = qv;
