@@ -116,9 +116,10 @@ def test_gpu_comb_matches_oracle(gpu_ctx_ntsc):
 
 @pytest.mark.gpu
 def test_gpu_comb_default_kernels_equal_option_kernels(monkeypatch):
-    """At comb-ntsc's defaults the library runs comb kernels with the options folded in as
-    constants; the option-taking kernels (LDG_COMB_GENERIC=1, read at context creation)
-    must give the same rgb48 bit for bit."""
+    """At comb-ntsc's defaults the library runs one fused row kernel with the options folded
+    in as constants; its FilterIQ fallback, the three-kernel path (LDG_COMB_UNFUSED=1) and
+    the option-taking kernels (LDG_COMB_GENERIC=1; all read at context creation) must give
+    the same rgb48 bit for bit."""
     from ldgpu import native
     from ldgpu.rfparams import RFTables
     rf = RFTables('NTSC')
@@ -127,14 +128,20 @@ def test_gpu_comb_default_kernels_equal_option_kernels(monkeypatch):
     noisy[:, :2] = frame_solid(45.0)[:, :2]
     fr = np.stack([frame_solid(40.0, 1500, -900), np.clip(noisy, 0, 65535).astype(np.uint16)])
     out = []
-    for generic in ('0', '1'):
-        monkeypatch.setenv('LDG_COMB_GENERIC', generic)
+    # the fused row kernel (default), its FilterIQ fallback forced (warm-up 2: almost every
+    # lane's check fails), the three default kernels, the option-taking kernels
+    for env in ({}, {'LDG_COMB_IQW': '2'}, {'LDG_COMB_UNFUSED': '1'}, {'LDG_COMB_GENERIC': '1'}):
+        for k in ('LDG_COMB_IQW', 'LDG_COMB_UNFUSED', 'LDG_COMB_GENERIC'):
+            monkeypatch.delenv(k, raising=False)
+        for k, v in env.items():
+            monkeypatch.setenv(k, v)
         ctx = native.Context('NTSC', 0, max_reads=8)
         ctx.set_filters(rf.params(), rf.tables)
         ctx.comb_reset()
         out.append(ctx.comb_ntsc(fr))
         ctx.close()
-    assert np.array_equal(out[0], out[1])
+    for o in out[1:]:
+        assert np.array_equal(out[0], o)
 
 
 @pytest.mark.gpu
