@@ -358,7 +358,10 @@ class ShardedWorkload:
                             '(1/%d each, HBM-resident windows, RCCL halo exchange): RF->demod->TBC->.tbc+.pcm%s'
                             % (self.seconds, self.world, self.world, '' if a.no_comb else '->2D comb rgb48'),
                 'frames_per_step_rank0': frames // max(a.steps, 1), 'batch_reads': a.batch,
-                'parallelism': 'field-group sharded x%d' % self.world, 'io': 'HBM-resident'}
+                'parallelism': 'field-group sharded x%d' % self.world, 'io': 'HBM-resident',
+                'comb_state': 'each rank combs from an uninitialised burst-level EMA; lddecode.py re-combs the '
+                              'first frame(s) from the exact state after the exchange (shard.comb_fix), '
+                              'not timed here'}
 
     def checks(self):
         return {'frames_per_step_all_ranks': self.stats.get('frames_total'),
