@@ -268,10 +268,22 @@ extern "C" __global__ __launch_bounds__(256) void ldg_k_comb_burst(const uint16_
   const int total = n * chain;
   for (int p0 = 0; p0 < total; p0 += BURST_PIECE) {
     const int cnt = (total - p0) < BURST_PIECE ? (total - p0) : BURST_PIECE;
-    for (int k = tid; k < cnt; k += 256) {
-      const int j = p0 + k;
-      const int f = j / chain, l = firstline + j % chain;
-      s_u[k] = frames[(size_t)f * IN_X * IN_Y + (size_t)l * IN_X + 1];
+    // one uint16 per line, 1820 B apart: issue 16 loads per thread before their LDS
+    // stores, so the staging costs a few memory latencies instead of one per line
+    for (int k0 = 0; k0 < cnt; k0 += 16 * 256) {
+      uint16_t v[16];
+#pragma unroll
+      for (int u = 0; u < 16; u++) {
+        const int k = k0 + u * 256 + tid;
+        const int j = p0 + k;
+        const int f = j / chain, l = firstline + j % chain;
+        v[u] = (k < cnt) ? frames[(size_t)f * IN_X * IN_Y + (size_t)l * IN_X + 1] : (uint16_t)0;
+      }
+#pragma unroll
+      for (int u = 0; u < 16; u++) {
+        const int k = k0 + u * 256 + tid;
+        if (k < cnt) s_u[k] = v[u];
+      }
     }
     if (tid == 0) s_bad = cnt;
     __syncthreads();
@@ -742,9 +754,14 @@ extern "C" __global__ __launch_bounds__(256) void ldg_k_comb_fused(const uint16_
                 "the fused kernel covers comb-ntsc's default options only");
   static_assert(64 * IQC >= IQ_NS, "one chunk per lane");
   __shared__ uint16_t s_raw[3][IN_X + 2];                // raw lines l-2, l, l+2
-  __shared__ double s_c[3][IN_X];                        // Split1D clp0; s_c[0]: AdjustY's Y afterwards
   __shared__ double s_cv[CV_STRIDE];                     // SplitIQ's signed chroma
-  __shared__ double s_iq[2][IQ_NS];                      // FilterIQ outputs (I, Q)
+  // Split1D's clp0 of the three lines; once cv is formed the same memory holds
+  // AdjustY's Y (h < 834) and the FilterIQ outputs (34.6 KiB in all: 4 workgroups per CU)
+  __shared__ double s_buf[3 * IN_X];
+  double (*s_c)[IN_X] = reinterpret_cast<double (*)[IN_X]>(s_buf);
+  double* s_y = s_buf;                                   // [0, 834)
+  double (*s_iq)[IQ_NS] = reinterpret_cast<double (*)[IQ_NS]>(s_buf + 840);
+  static_assert(840 + 2 * IQ_NS <= 3 * IN_X, "Y and the FilterIQ outputs share Split1D's buffer");
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int f = blockIdx.x / O::nrows;
   const int row = blockIdx.x % O::nrows;
@@ -792,6 +809,27 @@ extern "C" __global__ __launch_bounds__(256) void ldg_k_comb_fused(const uint16_
   }
   __syncthreads();
   const bool fiq = l >= 44;
+  // AdjustY over h in [66, 834) (the span DoYNR's taps reach from the output pixels):
+  // waves 2-3 while waves 0-1 run the FilterIQ chains (all four without them)
+  {
+    const int t0 = fiq ? tid - 128 : tid, nt = fiq ? 128 : 256;
+    if (t0 >= 0) {
+      for (int h = 66 + t0; h < 834; h += nt) {
+        const int p = h + 2;
+        const double yy = (p >= 4 && p < 840) ? (double)s_raw[1][p] : 0.0;
+        const double ii = held_i(s_cv, p), qq = held_q(s_cv, p);
+        double comp = 0;
+        switch (h & 3) {
+          case 0: comp = ii; break;
+          case 1: comp = -qq; break;
+          case 2: comp = -ii; break;
+          default: comp = qq; break;
+        }
+        if (invertphase) comp = -comp;
+        s_y[h] = yy + comp;
+      }
+    }
+  }
   if (fiq && wv < 2) {
     // FilterIQ chain q = wv (comb_iq_lane's arithmetic, feed k from cv[6 + 2k + q])
     const int q = wv;
@@ -841,23 +879,6 @@ extern "C" __global__ __launch_bounds__(256) void ldg_k_comb_fused(const uint16_
         s_iq[q][k] = yy;
       }
     }
-  }
-  __syncthreads();
-  // ---- AdjustY over h in [66, 834) (the span DoYNR's taps reach from the output pixels)
-  double* s_y = s_c[0];
-  for (int h = 66 + tid; h < 834; h += 256) {
-    const int p = h + 2;
-    const double yy = (p >= 4 && p < 840) ? (double)s_raw[1][p] : 0.0;
-    const double ii = held_i(s_cv, p), qq = held_q(s_cv, p);
-    double comp = 0;
-    switch (h & 3) {
-      case 0: comp = ii; break;
-      case 1: comp = -qq; break;
-      case 2: comp = -ii; break;
-      default: comp = qq; break;
-    }
-    if (invertphase) comp = -comp;
-    s_y[h] = yy + comp;
   }
   __syncthreads();
   // ---- DoYNR, ToRGB
