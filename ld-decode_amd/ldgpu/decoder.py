@@ -216,6 +216,7 @@ class GPUDecoder:
         self.boot_wide = os.environ.get('LDG_BOOT_WIDE', '1') == '1'   # +6.5% on the 60 s bench (tools/bootwide_ab.sh)
         self.miss_drain = os.environ.get('LDG_MISS_DRAIN', '1') == '1'
         self.grid_votes = int(os.environ.get('LDG_GRID_VOTES', '1'))   # _grid_next (1: the previous period's start)
+        self.hist_len = max(16, self.grid_votes * P + 2)                  # valid field starts the planner keeps
         self.plan_located = 0              # leading fields the last plan walked on decoded reads
         self.htrace = [] if os.environ.get('LDG_HOSTTRACE') else None   # (perf_counter, event, n): host timeline
         self.comb, self.comb_sink = False, None
@@ -419,6 +420,8 @@ class GPUDecoder:
         PAL launch wasted, profiles/r04_c_pal_waste_10s.txt); the vote keeps it to that read."""
         P, D = self.period, self.period_samples
         votes = votes or self.grid_votes
+        if votes == 1:
+            return starts[-(P - 1)] + D         # the planner's hot path (once per guessed read)
         counts, best, bestc = {}, None, 0
         for m in range(1, votes + 1):
             j = m * P - 1
@@ -840,7 +843,7 @@ class GPUDecoder:
                 fr.log = field_log_lines(self.field_log, self.sysp.name == 'NTSC') if self.frame_log else None
                 fr.index = done + len(frames)
                 frames.append(fr)
-                hist = (hist + [x.readsample for x in self.field_log if x.valid])[-48:]
+                hist = (hist + [x.readsample for x in self.field_log if x.valid])[-self.hist_len:]
             self.stats['replay_s'] += time.perf_counter() - t0
             if self.stats['batches'] % 32 == 0:
                 gc.collect(1)
