@@ -484,6 +484,23 @@ def decode_sharded(dec, rank, world, allgather, sink=None, start_frame=0, length
     resident: frames stay in HBM (benchmark mode) and frame is None.
     init: the chain state at start_sample (a later epoch, ShardedDecode); epoch_end: a dict
     that receives the exact state after the last output frame (ShardedDecode.end_state)."""
+    import gc
+    import time
+    # the cyclic collector stays off for the whole phase sequence, as the decode keeps it
+    # off (GPUDecoder.decode): a full collection over a shard's thousands of frame records
+    # landing inside the exchange or the audio phase cost 10-100 ms (profiles/r04_j)
+    gc_on = gc.isenabled()
+    gc.disable()
+    try:
+        return _decode_sharded(dec, rank, world, allgather, sink, start_frame, length, start_sample,
+                               whole_capture, spill_dir, resident, comb, stats, init, epoch_end)
+    finally:
+        if gc_on:
+            gc.enable()
+
+
+def _decode_sharded(dec, rank, world, allgather, sink, start_frame, length, start_sample, whole_capture,
+                    spill_dir, resident, comb, stats, init, epoch_end):
     import time
     t0 = time.perf_counter()
     sd = ShardedDecode(dec, rank, world, start_frame, length=length, start_sample=start_sample,
