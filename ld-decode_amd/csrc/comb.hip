@@ -261,6 +261,7 @@ extern "C" __global__ __launch_bounds__(256) void ldg_k_comb_burst(const uint16_
 
   __shared__ uint16_t s_u[BURST_PIECE];
   __shared__ double s_in[256], s_out[256];
+  __shared__ double s_fm[64], s_fc[64];                  // the sequential fix-up's per-line terms
   __shared__ int s_bad;
   const int tid = threadIdx.x;
   double a_in = state[0];
@@ -303,8 +304,53 @@ extern "C" __global__ __launch_bounds__(256) void ldg_k_comb_burst(const uint16_
     const int bad = s_bad;
     const int last = (cnt - 1) / L;                     // the thread holding the piece's last line
     if (bad < cnt) {
-      if (tid == 0) {
-        s_out[last] = burst_run(s_u, bad, cnt, s_out[bad / L - 1], abl + p0);
+      // the sequential chain from the verified state before the failed chunk, on wave 0:
+      // each lane forms one line's multiplier / addend (the level arithmetic and its test,
+      // off the dependency path), lane 0 chains 64 lines at a time with only the multiply
+      // and the add on the path (one thread doing it all ran ~120 cycles per line: the
+      // per-line level test went through the scalar unit inside the chain)
+      if (tid < 64) {
+        double a = s_out[bad / L - 1];
+        for (int k0 = bad; k0 < cnt; k0 += 64) {
+          const int k = k0 + tid;
+          double bk = 0.0, m = 1.0, c = 0.0;
+          if (k < cnt) {
+            bk = burst_level(s_u[k]);
+            if (bk > 3) { m = .99; c = bk * .01; }
+          }
+          s_fm[tid] = m;
+          s_fc[tid] = c;
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+          __builtin_amdgcn_wave_barrier();
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+          if (tid == 0) {
+            const int nb = (cnt - k0) < 64 ? (cnt - k0) : 64;
+            int j = 0;
+            for (; j < nb && a < 0; j++) {        // not yet initialised (the stream's first lines)
+              a = burst_step(a, s_u[k0 + j]);
+              abl[p0 + k0 + j] = a;
+            }
+#pragma unroll 1
+            for (; j + 16 <= nb; j += 16) {
+              double mm[16], cc[16];
+#pragma unroll
+              for (int u = 0; u < 16; u++) { mm[u] = s_fm[j + u]; cc[u] = s_fc[j + u]; }
+#pragma unroll
+              for (int u = 0; u < 16; u++) {
+                a = (a * mm[u]) + cc[u];
+                abl[p0 + k0 + j + u] = a;
+              }
+            }
+            for (; j < nb; j++) {
+              a = (a * s_fm[j]) + s_fc[j];
+              abl[p0 + k0 + j] = a;
+            }
+          }
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+          __builtin_amdgcn_wave_barrier();
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        }
+        if (tid == 0) s_out[last] = a;
       }
       __syncthreads();
     }
