@@ -802,36 +802,18 @@ extern "C" __global__ __launch_bounds__(256) void ldg_k_comb_out_opt(const uint1
 // 0.547^128 ~ 1e-34; LDG_COMB_IQW small forces the fallback in the tests).
 // grid: n * OUT_H workgroups of 256 threads.
 constexpr int IQC = 7;
-extern "C" __global__ __launch_bounds__(256) void ldg_k_comb_fused(const uint16_t* __restrict__ frames,
-                                                                   const double* __restrict__ abl,
-                                                                   uint16_t* __restrict__ rgb, int iqw) {
+// One row of the default 2D comb with its raw lines l-2, l, l+2 already in s_raw
+// (ldg_k_comb_fused, ldg_k_comb_rows).  Ends with every thread's stores issued;
+// s_raw, s_cv and s_buf may be rewritten after a __syncthreads.
+__device__ __forceinline__ void comb_row_default(const uint16_t (*s_raw)[IN_X + 2], double* s_cv, double* s_buf,
+                                                 int f, int row, double aburst, uint16_t* __restrict__ rgb, int iqw) {
   using O = CombDefaults;
-  static_assert(O::firstline >= 36 && O::firstline + O::nrows <= IN_Y - 2 && !O::wide && O::nr_c <= 0 &&
-                    O::colorlpf && !O::lpq && !O::bw,
-                "the fused kernel covers comb-ntsc's default options only");
-  static_assert(64 * IQC >= IQ_NS, "one chunk per lane");
-  __shared__ uint16_t s_raw[3][IN_X + 2];                // raw lines l-2, l, l+2
-  __shared__ double s_cv[CV_STRIDE];                     // SplitIQ's signed chroma
-  // Split1D's clp0 of the three lines; once cv is formed the same memory holds
-  // AdjustY's Y (h < 834) and the FilterIQ outputs (34.6 KiB in all: 4 workgroups per CU)
-  __shared__ double s_buf[3 * IN_X];
   double (*s_c)[IN_X] = reinterpret_cast<double (*)[IN_X]>(s_buf);
   double* s_y = s_buf;                                   // [0, 834)
   double (*s_iq)[IQ_NS] = reinterpret_cast<double (*)[IQ_NS]>(s_buf + 840);
   static_assert(840 + 2 * IQ_NS <= 3 * IN_X, "Y and the FilterIQ outputs share Split1D's buffer");
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const int f = blockIdx.x / O::nrows;
-  const int row = blockIdx.x % O::nrows;
   const int l = row + O::firstline;
-  const uint16_t* fr = frames + (size_t)f * IN_X * IN_Y;
-  for (int t = tid; t < 3 * (IN_X / 2); t += 256) {
-    const int k = t / (IN_X / 2), w = t % (IN_X / 2);
-    const int r = l - 2 + 2 * k;
-    const uint32_t v = reinterpret_cast<const uint32_t*>(fr + (size_t)r * IN_X)[w];
-    s_raw[k][2 * w] = (uint16_t)(v & 0xffff);
-    s_raw[k][2 * w + 1] = (uint16_t)(v >> 16);
-  }
-  __syncthreads();
   for (int h = tid; h < IN_X; h += 256) {
 #pragma unroll
     for (int k = 0; k < 3; k++) {
@@ -939,7 +921,6 @@ extern "C" __global__ __launch_bounds__(256) void ldg_k_comb_fused(const uint16_
   }
   __syncthreads();
   // ---- DoYNR, ToRGB
-  const double aburst = abl[(size_t)f * O::chain_lines() + (l - O::firstline)];
   const double m = O::bright_m;
   const double kc = 10 / aburst, kb = 100 / (100 - O::black_ire);
   uint16_t* out = rgb + ((size_t)f * O::out_rows + row) * OUT_W * 3;
@@ -968,5 +949,85 @@ extern "C" __global__ __launch_bounds__(256) void ldg_k_comb_fused(const uint16_
     out[x * 3 + 0] = (uint16_t)r;
     out[x * 3 + 1] = (uint16_t)g;
     out[x * 3 + 2] = (uint16_t)b;
+  }
+}
+
+extern "C" __global__ __launch_bounds__(256) void ldg_k_comb_fused(const uint16_t* __restrict__ frames,
+                                                                   const double* __restrict__ abl,
+                                                                   uint16_t* __restrict__ rgb, int iqw) {
+  using O = CombDefaults;
+  static_assert(O::firstline >= 36 && O::firstline + O::nrows <= IN_Y - 2 && !O::wide && O::nr_c <= 0 &&
+                    O::colorlpf && !O::lpq && !O::bw,
+                "the fused kernel covers comb-ntsc's default options only");
+  static_assert(64 * IQC >= IQ_NS, "one chunk per lane");
+  __shared__ uint16_t s_raw[3][IN_X + 2];                // raw lines l-2, l, l+2
+  __shared__ double s_cv[CV_STRIDE];                     // SplitIQ's signed chroma
+  // Split1D's clp0 of the three lines; once cv is formed the same memory holds
+  // AdjustY's Y (h < 834) and the FilterIQ outputs (34.6 KiB in all: 4 workgroups per CU)
+  __shared__ double s_buf[3 * IN_X];
+  const int tid = threadIdx.x;
+  const int f = blockIdx.x / O::nrows;
+  const int row = blockIdx.x % O::nrows;
+  const int l = row + O::firstline;
+  const uint16_t* fr = frames + (size_t)f * IN_X * IN_Y;
+  for (int t = tid; t < 3 * (IN_X / 2); t += 256) {
+    const int k = t / (IN_X / 2), w = t % (IN_X / 2);
+    const int r = l - 2 + 2 * k;
+    const uint32_t v = reinterpret_cast<const uint32_t*>(fr + (size_t)r * IN_X)[w];
+    s_raw[k][2 * w] = (uint16_t)(v & 0xffff);
+    s_raw[k][2 * w + 1] = (uint16_t)(v >> 16);
+  }
+  __syncthreads();
+  comb_row_default(s_raw, s_cv, s_buf, f, row, abl[(size_t)f * O::chain_lines() + (l - O::firstline)], rgb, iqw);
+}
+
+// ldg_k_comb_rows: the same rows from a persistent grid of G workgroups, row
+// r = blockIdx.x + G i.  A row workgroup spends most of its life waiting on its
+// three raw-line loads, and any resident comb wave keeps a demod workgroup off
+// its CU; here the next row's lines (and its burst level) are loaded into
+// registers while the current row is computed, so each CU the comb holds is
+// busy computing.  grid: G x 256 (G <= rows).
+constexpr int COMB_PRE = (3 * (IN_X / 2) + 255) / 256;   // raw 32-bit words per thread per row
+extern "C" __global__ __launch_bounds__(256) void ldg_k_comb_rows(const uint16_t* __restrict__ frames,
+                                                                  const double* __restrict__ abl,
+                                                                  uint16_t* __restrict__ rgb, int iqw, int total) {
+  using O = CombDefaults;
+  __shared__ uint16_t s_raw[3][IN_X + 2];
+  __shared__ double s_cv[CV_STRIDE];
+  __shared__ double s_buf[3 * IN_X];
+  const int tid = threadIdx.x;
+  const int G = gridDim.x;
+  uint32_t pre[COMB_PRE];
+  double ab_pre = 0.0;
+  auto fetch = [&](int r) {
+    const int f = r / O::nrows, row = r % O::nrows, l = row + O::firstline;
+    const uint16_t* fr = frames + (size_t)f * IN_X * IN_Y;
+#pragma unroll
+    for (int q = 0; q < COMB_PRE; q++) {
+      const int t = tid + 256 * q;
+      if (t < 3 * (IN_X / 2)) {
+        const int k = t / (IN_X / 2), w = t % (IN_X / 2);
+        pre[q] = reinterpret_cast<const uint32_t*>(fr + (size_t)(l - 2 + 2 * k) * IN_X)[w];
+      }
+    }
+    ab_pre = abl[(size_t)f * O::chain_lines() + row];
+  };
+  int r = blockIdx.x;
+  if (r < total) fetch(r);
+  for (; r < total; r += G) {
+#pragma unroll
+    for (int q = 0; q < COMB_PRE; q++) {
+      const int t = tid + 256 * q;
+      if (t < 3 * (IN_X / 2)) {
+        const int k = t / (IN_X / 2), w = t % (IN_X / 2);
+        s_raw[k][2 * w] = (uint16_t)(pre[q] & 0xffff);
+        s_raw[k][2 * w + 1] = (uint16_t)(pre[q] >> 16);
+      }
+    }
+    const double aburst = ab_pre;
+    __syncthreads();
+    if (r + G < total) fetch(r + G);                     // in flight while this row is computed
+    comb_row_default(s_raw, s_cv, s_buf, r / O::nrows, r % O::nrows, aburst, rgb, iqw);
+    __syncthreads();                                     // s_raw / s_cv / s_buf free for the next row
   }
 }

@@ -117,9 +117,10 @@ def test_gpu_comb_matches_oracle(gpu_ctx_ntsc):
 @pytest.mark.gpu
 def test_gpu_comb_default_kernels_equal_option_kernels(monkeypatch):
     """At comb-ntsc's defaults the library runs one fused row kernel with the options folded
-    in as constants; its FilterIQ fallback, the three-kernel path (LDG_COMB_UNFUSED=1) and
-    the option-taking kernels (LDG_COMB_GENERIC=1; all read at context creation) must give
-    the same rgb48 bit for bit."""
+    in as constants, from a persistent grid (LDG_COMB_ROWS workgroups; 3: many rows each,
+    0: one workgroup per row); its FilterIQ fallback, the three-kernel path
+    (LDG_COMB_UNFUSED=1) and the option-taking kernels (LDG_COMB_GENERIC=1; all read at
+    context creation) must give the same rgb48 bit for bit."""
     from ldgpu import native
     from ldgpu.rfparams import RFTables
     rf = RFTables('NTSC')
@@ -130,8 +131,9 @@ def test_gpu_comb_default_kernels_equal_option_kernels(monkeypatch):
     out = []
     # the fused row kernel (default), its FilterIQ fallback forced (warm-up 2: almost every
     # lane's check fails), the three default kernels, the option-taking kernels
-    for env in ({}, {'LDG_COMB_IQW': '2'}, {'LDG_COMB_UNFUSED': '1'}, {'LDG_COMB_GENERIC': '1'}):
-        for k in ('LDG_COMB_IQW', 'LDG_COMB_UNFUSED', 'LDG_COMB_GENERIC'):
+    for env in ({}, {'LDG_COMB_ROWS': '3'}, {'LDG_COMB_ROWS': '0'}, {'LDG_COMB_IQW': '2'}, {'LDG_COMB_UNFUSED': '1'},
+                {'LDG_COMB_GENERIC': '1'}):
+        for k in ('LDG_COMB_ROWS', 'LDG_COMB_IQW', 'LDG_COMB_UNFUSED', 'LDG_COMB_GENERIC'):
             monkeypatch.delenv(k, raising=False)
         for k, v in env.items():
             monkeypatch.setenv(k, v)
