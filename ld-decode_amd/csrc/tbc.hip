@@ -521,7 +521,10 @@ __device__ __forceinline__ uint16_t tbc_pixel(double v, double wow, const SysCon
 #define LDG_FINAL_WAVES 6
 #endif
 // (6 waves per SIMD: 78 VGPRs, six line workgroups per CU, 138 KiB of LDS)
-extern "C" __global__ __launch_bounds__(FINAL_NT, LDG_FINAL_WAVES) void ldg_k_final_lines(
+// HOIST: the evaluation's two knot samples per output are loaded together with the
+// solve's samples (one memory round trip per line instead of two, for more VGPRs)
+template <bool HOIST>
+__device__ __forceinline__ void final_lines_impl(
     const int32_t* __restrict__ smap, const double* __restrict__ video, int64_t vread_stride, int64_t vchan_stride,
     SysConst C, FieldRec* __restrict__ recs, const double* __restrict__ lines, const float* __restrict__ blevel,
     uint16_t* __restrict__ pic, int64_t pic_stride) {
@@ -597,6 +600,27 @@ extern "C" __global__ __launch_bounds__(FINAL_NT, LDG_FINAL_WAVES) void ldg_k_fi
   double yv[FINAL_CHMAX + 2];
 #pragma unroll
   for (int q = 0; q < FINAL_CHMAX + 2; q++) yv[q] = (q < nq + 2) ? y[lo + t0 - 1 + q] : 0.0;
+  // ---- evaluation geometry: linspace(b - ib, (e - b) + (b - ib), W + 1)[:-1]
+  const double x0 = begin - (double)ib;
+  const double span = end - begin;
+  const double step = ((span + x0) - x0) / (double)W;
+  constexpr int NO = (MAX_OUTW + FINAL_NT - 1) / FINAL_NT;
+  auto knot = [&](int e) {
+    const int o = tid + FINAL_NT * e;
+    double x = (double)o * step;
+    x = x + x0;
+    int64_t j = (int64_t)floor(x);
+    return (int)(j < 0 ? 0 : (j > n - 1 ? n - 1 : j));
+  };
+  double yk[NO], yk1[NO];
+  if constexpr (HOIST) {
+#pragma unroll
+    for (int e = 0; e < NO; e++) {
+      const int o = tid + FINAL_NT * e, k = knot(e);
+      yk[e] = (o < W) ? y[k] : 0.0;
+      yk1[e] = (o < W) ? y[k + 1] : 0.0;
+    }
+  }
   __syncthreads();
   const double M1 = S.m1, Mn1 = S.mn1;
   const double BL = M1, BR = Mn1;
@@ -662,13 +686,8 @@ extern "C" __global__ __launch_bounds__(FINAL_NT, LDG_FINAL_WAVES) void ldg_k_fi
     ms[n] = 2.0 * Mn1 - ms[n - 2];
   }
   __syncthreads();
-  // ---- evaluation at W points: linspace(b - ib, (e - b) + (b - ib), W + 1)[:-1]
-  const double x0 = begin - (double)ib;
-  const double span = end - begin;
-  const double step = ((span + x0) - x0) / (double)W;
+  // ---- evaluation at W points
   const double wow = (end - begin) / (double)C.linelen;
-  constexpr int NO = (MAX_OUTW + FINAL_NT - 1) / FINAL_NT;
-  double yk[NO], yk1[NO];
   int kk[NO];
   double xs[NO];
 #pragma unroll
@@ -676,12 +695,13 @@ extern "C" __global__ __launch_bounds__(FINAL_NT, LDG_FINAL_WAVES) void ldg_k_fi
     const int o = tid + FINAL_NT * e;
     double x = (double)o * step;
     x = x + x0;
-    int64_t j = (int64_t)floor(x);
-    const int k = (int)(j < 0 ? 0 : (j > n - 1 ? n - 1 : j));
+    const int k = knot(e);
     kk[e] = k;
     xs[e] = x;
-    yk[e] = (o < W) ? y[k] : 0.0;
-    yk1[e] = (o < W) ? y[k + 1] : 0.0;
+    if constexpr (!HOIST) {
+      yk[e] = (o < W) ? y[k] : 0.0;
+      yk1[e] = (o < W) ? y[k + 1] : 0.0;
+    }
   }
 #pragma unroll
   for (int e = 0; e < NO; e++) {
@@ -703,6 +723,19 @@ extern "C" __global__ __launch_bounds__(FINAL_NT, LDG_FINAL_WAVES) void ldg_k_fi
     const double clevel = (1 / 1.45) / hzs;
     if (tid == 1) out[1] = (uint16_t)(327.67 * clevel * fabs((double)bl));
   }
+}
+
+extern "C" __global__ __launch_bounds__(FINAL_NT, LDG_FINAL_WAVES) void ldg_k_final_lines(
+    const int32_t* __restrict__ smap, const double* __restrict__ video, int64_t vread_stride, int64_t vchan_stride,
+    SysConst C, FieldRec* __restrict__ recs, const double* __restrict__ lines, const float* __restrict__ blevel,
+    uint16_t* __restrict__ pic, int64_t pic_stride) {
+  final_lines_impl<false>(smap, video, vread_stride, vchan_stride, C, recs, lines, blevel, pic, pic_stride);
+}
+extern "C" __global__ __launch_bounds__(FINAL_NT, 5) void ldg_k_final_lines_h(
+    const int32_t* __restrict__ smap, const double* __restrict__ video, int64_t vread_stride, int64_t vchan_stride,
+    SysConst C, FieldRec* __restrict__ recs, const double* __restrict__ lines, const float* __restrict__ blevel,
+    uint16_t* __restrict__ pic, int64_t pic_stride) {
+  final_lines_impl<true>(smap, video, vread_stride, vchan_stride, C, recs, lines, blevel, pic, pic_stride);
 }
 
 // Mark reads still pending after the whole chain as valid.
