@@ -261,7 +261,7 @@ extern "C" __global__ __launch_bounds__(256) void ldg_k_comb_burst(const uint16_
 
   __shared__ uint16_t s_u[BURST_PIECE];
   __shared__ double s_in[256], s_out[256];
-  __shared__ double s_fm[64], s_fc[64];                  // the sequential fix-up's per-line terms
+  __shared__ double s_fm[BURST_PIECE / 256], s_fc[BURST_PIECE / 256];   // the fix-up's per-line terms (one chunk)
   __shared__ int s_bad, s_stop;
   const int tid = threadIdx.x;
   double a_in = state[0];
@@ -313,54 +313,63 @@ extern "C" __global__ __launch_bounds__(256) void ldg_k_comb_burst(const uint16_
       // from there every chunk whose start check passed is exact, so it resumes only at
       // the next failed boundary.
       if (tid < 64) {
-        int jb = bad / L;                                // the failed chunk
-        double a = s_out[jb - 1];                        // exact (the chunks before jb are)
-        while (jb * L < cnt) {
-          int stop = cnt;
-          for (int k0 = jb * L; k0 < cnt && stop == cnt; k0 += 64) {
-            const int k = k0 + tid;
-            double m = 1.0, c = 0.0;
-            if (k < cnt) {
-              const double bk = burst_level(s_u[k]);
-              if (bk > 3) { m = .99; c = bk * .01; }
+        int q = bad / L;                                 // the failed chunk
+        double a = s_out[q - 1];                         // exact (the chunks before q are)
+        while (q <= last) {
+          bool met = false;
+          for (; q <= last && !met; q++) {
+            const int k0 = q * L, k1 = (k0 + L) < cnt ? k0 + L : cnt;
+            for (int kk = k0 + tid; kk < k1; kk += 64) {
+              const double bk = burst_level(s_u[kk]);
+              const bool qual = bk > 3;
+              s_fm[kk - k0] = qual ? .99 : 1.0;
+              s_fc[kk - k0] = qual ? bk * .01 : 0.0;
             }
-            s_fm[tid] = m;
-            s_fc[tid] = c;
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
             if (tid == 0) {
-              const int nb = (cnt - k0) < 64 ? (cnt - k0) : 64;
-              int st = cnt;
-              for (int j = 0; j < nb; j++) {
-                const int kk = k0 + j;
-                if (a < 0) a = burst_step(a, s_u[kk]);   // not yet initialised (the stream's first lines)
-                else a = (a * s_fm[j]) + s_fc[j];
-                abl[p0 + kk] = a;
-                if ((kk + 1) % L == 0 || kk + 1 == cnt) {
-                  if (__double_as_longlong(a) == __double_as_longlong(s_out[kk / L])) { st = kk + 1; break; }
+              const int nb = k1 - k0;
+              int j = 0;
+              for (; j < nb && a < 0; j++) {             // not yet initialised (the stream's first lines)
+                a = burst_step(a, s_u[k0 + j]);
+                abl[p0 + k0 + j] = a;
+              }
+#pragma unroll 1
+              for (; j + 16 <= nb; j += 16) {
+                double mm[16], cc[16];
+#pragma unroll
+                for (int u = 0; u < 16; u++) { mm[u] = s_fm[j + u]; cc[u] = s_fc[j + u]; }
+#pragma unroll
+                for (int u = 0; u < 16; u++) {
+                  a = (a * mm[u]) + cc[u];
+                  abl[p0 + k0 + j + u] = a;
                 }
               }
-              s_stop = st;
+              for (; j < nb; j++) {
+                a = (a * s_fm[j]) + s_fc[j];
+                abl[p0 + k0 + j] = a;
+              }
+              s_stop = __double_as_longlong(a) == __double_as_longlong(s_out[q]);
             }
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-            stop = s_stop;
+            met = s_stop != 0;
           }
-          if (stop >= cnt) {
+          if (!met) {                                    // ran to the piece's end
             if (tid == 0) s_out[last] = a;
             break;
           }
-          // the next failed boundary at or after chunk stop / L (its start check against
-          // the now-exact speculative end before it)
+          // the exact state after chunk q - 1 is its speculative end: chunks from q on are
+          // exact up to the next failed start check
           int nxt = 256;
-          for (int q = stop / L + tid; q <= last; q += 64)
-            if (q > 0 && __double_as_longlong(s_in[q]) != __double_as_longlong(s_out[q - 1])) { nxt = q; break; }
+          for (int m = q + tid; m <= last; m += 64)
+            if (__double_as_longlong(s_in[m]) != __double_as_longlong(s_out[m - 1])) { nxt = m; break; }
           for (int o = 32; o > 0; o >>= 1) nxt = min(nxt, __shfl_xor(nxt, o));
           if (nxt > last) break;                         // s_out[last] is exact already
-          jb = nxt;
-          a = s_out[jb - 1];
+          q = nxt;
+          a = s_out[q - 1];
         }
       }
       __syncthreads();
