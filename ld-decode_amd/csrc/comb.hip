@@ -836,6 +836,7 @@ __device__ __forceinline__ void comb_row_default(const uint16_t (*s_raw)[IN_X + 
     }
   }
   __syncthreads();
+  KSTAMP(0, 2);
   const bool invertphase = (s_raw[1][0] == 16384);
   for (int h = tid; h < CV_STRIDE; h += 256) {
     double cv = 0.0;
@@ -856,6 +857,7 @@ __device__ __forceinline__ void comb_row_default(const uint16_t (*s_raw)[IN_X + 
     s_cv[h] = cv;
   }
   __syncthreads();
+  KSTAMP(0, 3);
   const bool fiq = l >= 44;
   // AdjustY over h in [66, 834) (the span DoYNR's taps reach from the output pixels):
   // waves 2-3 while waves 0-1 run the FilterIQ chains (all four without them)
@@ -929,6 +931,7 @@ __device__ __forceinline__ void comb_row_default(const uint16_t (*s_raw)[IN_X + 
     }
   }
   __syncthreads();
+  KSTAMP(0, 4);
   // ---- DoYNR, ToRGB
   const double m = O::bright_m;
   const double kc = 10 / aburst, kb = 100 / (100 - O::black_ire);
@@ -959,6 +962,7 @@ __device__ __forceinline__ void comb_row_default(const uint16_t (*s_raw)[IN_X + 
     out[x * 3 + 1] = (uint16_t)g;
     out[x * 3 + 2] = (uint16_t)b;
   }
+  KSTAMP(0, 5);
 }
 
 extern "C" __global__ __launch_bounds__(256) void ldg_k_comb_fused(const uint16_t* __restrict__ frames,
@@ -974,6 +978,7 @@ extern "C" __global__ __launch_bounds__(256) void ldg_k_comb_fused(const uint16_
   // Split1D's clp0 of the three lines; once cv is formed the same memory holds
   // AdjustY's Y (h < 834) and the FilterIQ outputs (34.6 KiB in all: 4 workgroups per CU)
   __shared__ double s_buf[3 * IN_X];
+  KSTAMP(0, 0);
   const int tid = threadIdx.x;
   const int f = blockIdx.x / O::nrows;
   const int row = blockIdx.x % O::nrows;
@@ -987,6 +992,7 @@ extern "C" __global__ __launch_bounds__(256) void ldg_k_comb_fused(const uint16_
     s_raw[k][2 * w + 1] = (uint16_t)(v >> 16);
   }
   __syncthreads();
+  KSTAMP(0, 1);
   comb_row_default(s_raw, s_cv, s_buf, f, row, abl[(size_t)f * O::chain_lines() + (l - O::firstline)], rgb, iqw);
 }
 

@@ -15,7 +15,7 @@ import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, 'ld-decode_amd'))
 VARIANT = os.path.join(ROOT, 'ld-decode_amd', 'ldgpu', 'libldgpu_stamps.so')
-KERNELS = ['comb_rows', 'final_lines', 'burst_field', 'sync', 'burst_lines', 'philips']
+KERNELS = ['comb_fused', 'final_lines', 'burst_field', 'sync', 'burst_lines', 'philips']
 NK, NB, NP = 6, 4096, 16
 
 
