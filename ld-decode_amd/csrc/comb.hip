@@ -899,8 +899,20 @@ __device__ __forceinline__ void comb_row_default(const uint16_t (*s_raw)[IN_X + 
     const int kw = (k0 - iqw > 0) ? k0 - iqw : 0;
     double y = 0.0, x1 = xin(kw - 1);
     if (k0 < IQ_NS) {
-#pragma unroll 8
-      for (int k = kw; k < k0; k++) {
+      // 8 feeds read ahead of their steps: only the multiply-subtract on y is on the chain
+      int k = kw;
+#pragma unroll 1
+      for (; k + 8 <= k0; k += 8) {
+        double xs[8];
+#pragma unroll
+        for (int u = 0; u < 8; u++) xs[u] = xin(k + u);
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+          y = step(xs[u], x1, y);
+          x1 = xs[u];
+        }
+      }
+      for (; k < k0; k++) {
         const double x = xin(k);
         y = step(x, x1, y);
         x1 = x;
@@ -908,13 +920,15 @@ __device__ __forceinline__ void comb_row_default(const uint16_t (*s_raw)[IN_X + 
     }
     const double y_in = y;
     if (k0 < IQ_NS) {
+      double xs[IQC];
 #pragma unroll
-      for (int k = k0; k < k0 + IQC; k++) {
-        if (k < k1) {
-          const double x = xin(k);
-          y = step(x, x1, y);
-          x1 = x;
-          s_iq[q][k] = y;
+      for (int u = 0; u < IQC; u++) xs[u] = (k0 + u < k1) ? xin(k0 + u) : 0.0;
+#pragma unroll
+      for (int u = 0; u < IQC; u++) {
+        if (k0 + u < k1) {
+          y = step(xs[u], x1, y);
+          x1 = xs[u];
+          s_iq[q][k0 + u] = y;
         }
       }
     }
