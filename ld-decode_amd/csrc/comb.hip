@@ -123,11 +123,15 @@ __device__ __forceinline__ double clampd(double v, double lo, double hi) { retur
 
 // clp1 with the three clp0 rows staged in LDS (p = l-2, c = l, n = l+2; the
 // PAL decoder passes l-4 / l+4 and its own p_2drange = 45 * its irescale).
+__device__ __forceinline__ double clp1_v(double c0, double cm, double p0, double pm, double n0, double nm,
+                                         double p2drange = P_2DRANGE, bool adaptive = true);
 __device__ __forceinline__ double clp1_lds(const double* p1, const double* c1, const double* n1, int h,
                                            double p2drange = P_2DRANGE, bool adaptive = true) {
-  const double c0 = c1[h], cm = c1[h - 1];
-  const double p0 = p1[h], pm = p1[h - 1];
-  const double n0 = n1[h], nm = n1[h - 1];
+  return clp1_v(c1[h], c1[h - 1], p1[h], p1[h - 1], n1[h], n1[h - 1], p2drange, adaptive);
+}
+// the same from the six clp0 values (line l at h / h-1, l-2, l+2)
+__device__ __forceinline__ double clp1_v(double c0, double cm, double p0, double pm, double n0, double nm,
+                                         double p2drange, bool adaptive) {
   double kp = fabs(fabs(c0) - fabs(p0));
   kp += fabs(fabs(cm) - fabs(pm));
   kp -= (fabs(c0) + fabs(cm)) * .10;
@@ -817,38 +821,31 @@ constexpr int IQC = 7;
 __device__ __forceinline__ void comb_row_default(const uint16_t (*s_raw)[IN_X + 2], double* s_cv, double* s_buf,
                                                  int f, int row, double aburst, uint16_t* __restrict__ rgb, int iqw) {
   using O = CombDefaults;
-  double (*s_c)[IN_X] = reinterpret_cast<double (*)[IN_X]>(s_buf);
   double* s_y = s_buf;                                   // [0, 834)
   double (*s_iq)[IQ_NS] = reinterpret_cast<double (*)[IQ_NS]>(s_buf + 840);
-  static_assert(840 + 2 * IQ_NS <= 3 * IN_X, "Y and the FilterIQ outputs share Split1D's buffer");
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int l = row + O::firstline;
-  for (int h = tid; h < IN_X; h += 256) {
-#pragma unroll
-    for (int k = 0; k < 3; k++) {
-      const int r = l - 2 + 2 * k;
-      double c = 0.0;
-      if (r >= 44 && h >= 4 && h < 840) {
-        const int avg = ((int)s_raw[k][h + 2] + (int)s_raw[k][h - 2]) / 2;   // integer average (Split1D)
-        c = (double)(avg - (int)s_raw[k][h]);
-      }
-      s_c[k][h] = c;
-    }
-  }
-  __syncthreads();
   KSTAMP(0, 2);
+  // Split1D's clp0 of the three lines, formed where Split2D reads it (no staging pass)
+  auto clp0 = [&](int k, int h) -> double {
+    const int r = l - 2 + 2 * k;
+    if (r < 44 || h < 4 || h >= 840) return 0.0;
+    const int avg = ((int)s_raw[k][h + 2] + (int)s_raw[k][h - 2]) / 2;   // integer average (Split1D)
+    return (double)(avg - (int)s_raw[k][h]);
+  };
   const bool invertphase = (s_raw[1][0] == 16384);
   for (int h = tid; h < CV_STRIDE; h += 256) {
     double cv = 0.0;
     if (h >= 4 && h < 840) {
       double cavg = 0;
       cavg += 0.0 * 0.0;                                 // clpbuffer[2] * combk[2]
+      const double c1h = clp0(1, h);
       if (h >= 18) {
-        cavg += clp1_lds(s_c[0], s_c[1], s_c[2], h, P_2DRANGE, true) * 1.0;
-        cavg += s_c[1][h] * 0.0;
+        cavg += clp1_v(c1h, clp0(1, h - 1), clp0(0, h), clp0(0, h - 1), clp0(2, h), clp0(2, h - 1), P_2DRANGE, true) * 1.0;
+        cavg += c1h * 0.0;
       } else {
         cavg += 0.0 * 0.0;
-        cavg += s_c[1][h] * 1.0;
+        cavg += c1h * 1.0;
       }
       cavg /= 2;
       if (!invertphase) cavg = -cavg;
@@ -989,9 +986,8 @@ extern "C" __global__ __launch_bounds__(256) void ldg_k_comb_fused(const uint16_
   static_assert(64 * IQC >= IQ_NS, "one chunk per lane");
   __shared__ uint16_t s_raw[3][IN_X + 2];                // raw lines l-2, l, l+2
   __shared__ double s_cv[CV_STRIDE];                     // SplitIQ's signed chroma
-  // Split1D's clp0 of the three lines; once cv is formed the same memory holds
-  // AdjustY's Y (h < 834) and the FilterIQ outputs (34.6 KiB in all: 4 workgroups per CU)
-  __shared__ double s_buf[3 * IN_X];
+  // AdjustY's Y (h < 834) and the FilterIQ outputs (26.3 KiB of LDS in all: 6 workgroups per CU)
+  __shared__ double s_buf[840 + 2 * IQ_NS];
   KSTAMP(0, 0);
   const int tid = threadIdx.x;
   const int f = blockIdx.x / O::nrows;
@@ -1023,7 +1019,7 @@ extern "C" __global__ __launch_bounds__(256) void ldg_k_comb_rows(const uint16_t
   using O = CombDefaults;
   __shared__ uint16_t s_raw[3][IN_X + 2];
   __shared__ double s_cv[CV_STRIDE];
-  __shared__ double s_buf[3 * IN_X];
+  __shared__ double s_buf[840 + 2 * IQ_NS];
   const int tid = threadIdx.x;
   const int G = gridDim.x;
   uint32_t pre[COMB_PRE];
