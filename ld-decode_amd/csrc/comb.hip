@@ -811,8 +811,8 @@ extern "C" __global__ __launch_bounds__(256) void ldg_k_comb_out_opt(const uint1
 // that reaches feed 0) and its chunk is the sequential chain's iff its state
 // entering the chunk equals lane j - 1's final state; any failed check reruns
 // the whole chain on one lane.  Every arithmetic step is comb_iq's, so the
-// output is bit-identical to the three-kernel path.  iqw: the warm-up (128,
-// 0.547^128 ~ 1e-34; LDG_COMB_IQW small forces the fallback in the tests).
+// output is bit-identical to the three-kernel path.  iqw: the exact warm-up from an
+// affine-scan seed (28 feeds; LDG_COMB_IQW=0 forces the fallback in the tests).
 // grid: n * OUT_H workgroups of 256 threads.
 constexpr int IQC = 7;
 // One row of the default 2D comb with its raw lines l-2, l, l+2 already in s_raw
@@ -893,20 +893,60 @@ __device__ __forceinline__ void comb_row_default(const uint16_t (*s_raw)[IN_X + 
       return ya;
     };
     const int k0 = lane * IQC, k1 = (k0 + IQC < IQ_NS) ? k0 + IQC : IQ_NS;
-    const int kw = (k0 - iqw > 0) ? k0 - iqw : 0;
-    double y = 0.0, x1 = xin(kw - 1);
+    // the chunk's feeds, read once
+    double xs[IQC];
+#pragma unroll
+    for (int u = 0; u < IQC; u++) xs[u] = (k0 + u < k1) ? xin(k0 + u) : 0.0;
+    // Seed: the chunk maps y -> A y + B composed across the lanes (an affine scan) give
+    // every chunk start's state to within rounding; from the seed iqw feeds back (whole
+    // chunks) the exact steps run up to the chunk, and by then the seed's error has
+    // shrunk by 0.547^iqw (iqw 28: ~5e-8 of an ulp), so the states agree bit for bit --
+    // which the neighbour check below still verifies.
+    const int wch = (iqw + IQC - 1) / IQC;               // warm-up in whole chunks
+    const int kw = (lane - wch > 0) ? (lane - wch) * IQC : 0;
+    double y = 0.0;
+    {
+      const double alpha = -(LPI_A1 / 1.0);
+      double A = 1.0, B = 0.0, xp = xin(k0 - 1);
+#pragma unroll
+      for (int u = 0; u < IQC; u++) {
+        if (k0 + u < k1) {
+          double c = 0;
+          c += (LPI_B0 / 1.0) * xs[u];
+          c += (LPI_B1 / 1.0) * xp;
+          A = alpha * A;
+          B = alpha * B + c;
+          xp = xs[u];
+        }
+      }
+      // inclusive Kogge-Stone over the lanes: (A, B) = mine after theirs
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const double At = __shfl_up(A, o), Bt = __shfl_up(B, o);
+        if (lane >= o) {
+          B = A * Bt + B;
+          A = A * At;
+        }
+      }
+      // the state entering lane j's chunk is lane j-1's inclusive B (y_{-1} = 0); the
+      // warm-up starts at lane (j - wch)'s chunk, entered with lane (j - wch - 1)'s B
+      const int src = lane - wch - 1;
+      const double seed = __shfl(B, src < 0 ? 0 : src);
+      if (kw > 0) y = seed;
+    }
+    double x1 = xin(kw - 1);
     if (k0 < IQ_NS) {
       // 8 feeds read ahead of their steps: only the multiply-subtract on y is on the chain
       int k = kw;
 #pragma unroll 1
       for (; k + 8 <= k0; k += 8) {
-        double xs[8];
+        double xw[8];
 #pragma unroll
-        for (int u = 0; u < 8; u++) xs[u] = xin(k + u);
+        for (int u = 0; u < 8; u++) xw[u] = xin(k + u);
 #pragma unroll
         for (int u = 0; u < 8; u++) {
-          y = step(xs[u], x1, y);
-          x1 = xs[u];
+          y = step(xw[u], x1, y);
+          x1 = xw[u];
         }
       }
       for (; k < k0; k++) {
@@ -917,9 +957,6 @@ __device__ __forceinline__ void comb_row_default(const uint16_t (*s_raw)[IN_X + 
     }
     const double y_in = y;
     if (k0 < IQ_NS) {
-      double xs[IQC];
-#pragma unroll
-      for (int u = 0; u < IQC; u++) xs[u] = (k0 + u < k1) ? xin(k0 + u) : 0.0;
 #pragma unroll
       for (int u = 0; u < IQC; u++) {
         if (k0 + u < k1) {
