@@ -834,7 +834,11 @@ __device__ __forceinline__ void comb_row_default(const uint16_t (*s_raw)[IN_X + 
     return (double)(avg - (int)s_raw[k][h]);
   };
   const bool invertphase = (s_raw[1][0] == 16384);
-  for (int h = tid; h < CV_STRIDE; h += 256) {
+  // (unrolled: the pixels' dependent clp1 chains -- three divisions each -- interleave)
+#pragma unroll
+  for (int u = 0; u < (CV_STRIDE + 255) / 256; u++) {
+    const int h = tid + 256 * u;
+    if (h >= CV_STRIDE) continue;
     double cv = 0.0;
     if (h >= 4 && h < 840) {
       double cavg = 0;
@@ -984,7 +988,10 @@ __device__ __forceinline__ void comb_row_default(const uint16_t (*s_raw)[IN_X + 
   const double m = O::bright_m;
   const double kc = 10 / aburst, kb = 100 / (100 - O::black_ire);
   uint16_t* out = rgb + ((size_t)f * O::out_rows + row) * OUT_W * 3;
-  for (int x = tid; x < OUT_W; x += 256) {
+#pragma unroll
+  for (int u = 0; u < (OUT_W + 255) / 256; u++) {
+    const int x = tid + 256 * u;
+    if (x >= OUT_W) continue;
     const int h = x + OUT_X0;
     double y0 = 0;
 #pragma unroll
