@@ -584,6 +584,7 @@ __device__ __forceinline__ void final_lines_impl(
   }
   const int n = (int)n64;
   const double* y = dm + ib;
+  KSTAMP(1, 0);
   if (tid < 17) S.ct[tid] = g_ctab.v[tid];
   if (tid == 0) {
     S.m1 = (6.0 * ((y[2] - y[1]) - (y[1] - y[0]))) / 6.0;
@@ -622,6 +623,7 @@ __device__ __forceinline__ void final_lines_impl(
     }
   }
   __syncthreads();
+  KSTAMP(1, 1);
   const double M1 = S.m1, Mn1 = S.mn1;
   const double BL = M1, BR = Mn1;
   auto ct = [&](int t) { return t < 16 ? S.ct[t] : kCtInf; };
@@ -650,6 +652,7 @@ __device__ __forceinline__ void final_lines_impl(
     }
   }
   double dprev = block_affine_carry<FINAL_NT, false>(A, B, tid, S);
+  KSTAMP(1, 2);
 #pragma unroll
   for (int q = 0; q < FINAL_CHMAX; q++) {
     if (q < nq) {
@@ -669,6 +672,7 @@ __device__ __forceinline__ void final_lines_impl(
     }
   }
   double Mnext = block_affine_carry<FINAL_NT, true>(A, B, tid, S);
+  KSTAMP(1, 3);
   double* ms = S.ms;
 #pragma unroll
   for (int q = FINAL_CHMAX - 1; q >= 0; q--) {
@@ -686,6 +690,7 @@ __device__ __forceinline__ void final_lines_impl(
     ms[n] = 2.0 * Mn1 - ms[n - 2];
   }
   __syncthreads();
+  KSTAMP(1, 4);
   // ---- evaluation at W points
   const double wow = (end - begin) / (double)C.linelen;
   int kk[NO];
@@ -715,6 +720,7 @@ __device__ __forceinline__ void final_lines_impl(
     const double v = m6 * a * a * a + m16 * b * b * b + (yk[e] - m6) * a + (yk1[e] - m16) * b;
     out[o] = tbc_pixel(v, wow, C);
   }
+  KSTAMP(1, 5);
   // NTSC burst flag pixels (threads 0 / 1 wrote pixels 0 / 1 above)
   if (!pal && tid < 2 && row >= 1 && row < lc - 1) {
     const float bl = blevel[(int64_t)slot * MAX_LINES + row];
