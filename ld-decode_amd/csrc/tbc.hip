@@ -112,10 +112,33 @@ __device__ __forceinline__ double block_affine_carry(double A, double B, int tid
   const double exB = dpp_f64_or<SUFFIX ? 0x101 : 0x111>(B, 0.0);
   __syncthreads();
   double rb = 0.0;
-  if (SUFFIX) {
-    for (int r = NR - 1; r > row; r--) rb = S.ra[r] * rb + S.rb[r];
+  if constexpr (NR <= 4) {
+    if (SUFFIX) {
+      for (int r = NR - 1; r > row; r--) rb = S.ra[r] * rb + S.rb[r];
+    } else {
+      for (int r = 0; r < row; r++) rb = S.ra[r] * rb + S.rb[r];
+    }
   } else {
-    for (int r = 0; r < row; r++) rb = S.ra[r] * rb + S.rb[r];
+    // the row totals' carries by a Kogge-Stone on wave 0 (one dependent step per doubling
+    // instead of one per earlier row), written back over S.rb
+    if (tid < 64) {
+      double a = 1.0, b = 0.0;
+      if (tid < NR) { a = S.ra[tid]; b = S.rb[tid]; }
+#pragma unroll
+      for (int o = 1; o < NR; o <<= 1) {
+        const double at = SUFFIX ? __shfl_down(a, o) : __shfl_up(a, o);
+        const double bt = SUFFIX ? __shfl_down(b, o) : __shfl_up(b, o);
+        if (SUFFIX ? (tid + o < NR) : (tid >= o)) {
+          b = a * bt + b;
+          a = a * at;
+        }
+      }
+      // exclusive: the neighbouring row's inclusive value (0 at the end)
+      const double ex = SUFFIX ? __shfl_down(b, 1) : __shfl_up(b, 1);
+      if (tid < NR) S.rb[tid] = (SUFFIX ? (tid == NR - 1) : (tid == 0)) ? 0.0 : ex;
+    }
+    __syncthreads();
+    rb = S.rb[row];
   }
   __syncthreads();
   return exA * rb + exB;
