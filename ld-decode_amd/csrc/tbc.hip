@@ -823,23 +823,35 @@ extern "C" __global__ __launch_bounds__(256) void ldg_k_audio_ds(
   }
 }
 
-// Framer.formatoutput: grid (n_frames, frame_lines) x 256.
+// Framer.formatoutput: grid (n_frames, ceil(frame_lines / FRAME_ROWS)) x 256, FRAME_ROWS
+// rows per workgroup (one row per workgroup was ~16k tiny workgroups per call, each
+// holding a CU for a load round trip), 32-bit copies when the line length is even.
+constexpr int FRAME_ROWS = 8;
 extern "C" __global__ __launch_bounds__(256) void ldg_k_frames(const int32_t* __restrict__ top,
                                                                const int32_t* __restrict__ bot,
                                                                const FieldRec* __restrict__ recs,
                                                                const uint16_t* __restrict__ pic, int64_t pic_stride,
                                                                SysConst C, uint16_t* __restrict__ out) {
   const int f = blockIdx.x;
-  const int row = blockIdx.y;
   const int W = C.outlinelen;
   const int ts = top[f], bs = bot[f];
   const int lt = recs[ts].linecount, lb = recs[bs].linecount;
   const int lc = ((lt < lb) ? lt : lb) * 2;
-  uint16_t* dst = out + ((int64_t)f * C.frame_lines + row) * W;
-  const uint16_t* src = nullptr;
-  if (row < lc) src = pic + (int64_t)((row & 1) ? bs : ts) * pic_stride + (int64_t)(row >> 1) * W;
-  else if (row == lc) src = pic + (int64_t)((lt >= lb) ? ts : bs) * pic_stride + (int64_t)(lc >> 1) * W;
-  for (int x = threadIdx.x; x < W; x += blockDim.x) dst[x] = src ? src[x] : 0;
+  for (int i = 0; i < FRAME_ROWS; i++) {
+    const int row = blockIdx.y * FRAME_ROWS + i;
+    if (row >= C.frame_lines) break;
+    uint16_t* dst = out + ((int64_t)f * C.frame_lines + row) * W;
+    const uint16_t* src = nullptr;
+    if (row < lc) src = pic + (int64_t)((row & 1) ? bs : ts) * pic_stride + (int64_t)(row >> 1) * W;
+    else if (row == lc) src = pic + (int64_t)((lt >= lb) ? ts : bs) * pic_stride + (int64_t)(lc >> 1) * W;
+    if ((W & 1) == 0 && (pic_stride & 1) == 0) {
+      uint32_t* d32 = reinterpret_cast<uint32_t*>(dst);
+      const uint32_t* s32 = reinterpret_cast<const uint32_t*>(src);
+      for (int x = threadIdx.x; x < W / 2; x += blockDim.x) d32[x] = src ? s32[x] : 0u;
+    } else {
+      for (int x = threadIdx.x; x < W; x += blockDim.x) dst[x] = src ? src[x] : 0;
+    }
+  }
 }
 
 // ---------------------------------------------------------------------------
