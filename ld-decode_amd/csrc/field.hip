@@ -780,16 +780,20 @@ extern "C" __global__ __launch_bounds__(64) void ldg_k_hsync_lines(
   const int slot = smap[blockIdx.x / MAX_LINES];
   const int i = blockIdx.x % MAX_LINES;
   FieldRec* R = recs + slot;
-  if (R->status != FS_PENDING) return;
-  if (i >= R->nlines) return;
-  // demod_05 as the demod stored it
-  const double* d05 = video + (int64_t)slot * vread_stride + (int64_t)CH_05 * vchan_stride;
-  const int64_t len = R->n_out;
   const double* L1 = lines + (int64_t)slot * LINES_STRIDE + LL1 * MAX_LINES;
   double* L2 = lines + (int64_t)slot * LINES_STRIDE + LL2 * MAX_LINES;
   int8_t* B = bad + (int64_t)slot * MAX_LINES;
+  // the record, the line's location and flag in one memory round trip
+  const int status = R->status, nl = R->nlines;
+  const int64_t len = R->n_out;
   const double v = L1[i];
-  const bool lb = B[i] != 0;
+  const int lbi = B[i];
+  asm volatile("" ::"v"(v), "v"(status), "v"(nl), "v"(lbi));
+  if (status != FS_PENDING) return;
+  if (i >= nl) return;
+  // demod_05 as the demod stored it
+  const double* d05 = video + (int64_t)slot * vread_stride + (int64_t)CH_05 * vchan_stride;
+  const bool lb = lbi != 0;
   double out;
   int flag;
   hsync_line(d05, len, C, i, v, lb, lane, s_tmp, out, flag);

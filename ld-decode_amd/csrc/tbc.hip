@@ -304,10 +304,13 @@ extern "C" __global__ __launch_bounds__(64) void ldg_k_burst_lines(
   const int slot = smap[blockIdx.x / MAX_LINES];
   const int l = blockIdx.x % MAX_LINES;
   FieldRec* R = recs + slot;
-  if (R->status != FS_PENDING) return;
-  const int nl = R->nlines, lc = R->linecount;
   double* LN = lines + (int64_t)slot * LINES_STRIDE;
   const double* li = LN + (pass == 0 ? LL2 : LL3) * MAX_LINES;
+  // the record and the line's two locations in one memory round trip (clamped indices)
+  const int status = R->status, nl = R->nlines, lc = R->linecount;
+  const double b0 = li[l], b1 = li[l + 1 < MAX_LINES ? l + 1 : MAX_LINES - 1];
+  asm volatile("" ::"v"(b0), "v"(b1), "v"(status), "v"(nl), "v"(lc));
+  if (status != FS_PENDING) return;
   double* pv0 = LN + PAVG0 * MAX_LINES;
   double* pv1 = LN + PAVG1 * MAX_LINES;
   float* lvl = blevel + (int64_t)slot * MAX_LINES;
@@ -318,7 +321,6 @@ extern "C" __global__ __launch_bounds__(64) void ldg_k_burst_lines(
   }
   // demod_burst from the demod channel and the demod's per-chunk states (chan.hpp)
   const BurstSrc bur(bst, video + (int64_t)slot * vread_stride + (int64_t)CH_DEMOD * vchan_stride, slot, C);
-  const double b0 = li[l], b1 = li[l + 1];
   const double wow = (b1 - b0) / (double)C.linelen;
   const int W = C.outlinelen;
   const int rc = spline_block<64, 4>(bur, R->n_out, b0, b1, W, 20, 60, lane, S,
@@ -561,17 +563,20 @@ __device__ __forceinline__ void final_lines_impl(
   const int slot = smap[blockIdx.x / MAX_LINES];
   const int row = blockIdx.x % MAX_LINES;
   FieldRec* R = recs + slot;
-  if (R->status != FS_PENDING) return;
-  const int lc = R->linecount;
-  if (row >= lc) return;
   const int loff = (C.system == 1) ? 3 : 1;
   const int l = row + loff;
   const double* lf = lines + (int64_t)slot * LINES_STRIDE + LLF * MAX_LINES;
-  const double* dm = video + (int64_t)slot * vread_stride + (int64_t)CH_DEMOD * vchan_stride;
+  // the record and the line's two locations in one memory round trip (the locations
+  // are read before the record says the row is live: indices clamped into the array)
+  const int status = R->status, lc = R->linecount;
   const int64_t len = R->n_out;
+  const double begin = lf[l < MAX_LINES ? l : MAX_LINES - 1], end = lf[l + 1 < MAX_LINES ? l + 1 : MAX_LINES - 1];
+  asm volatile("" ::"v"(begin), "v"(end), "v"(status), "v"(lc));
+  if (status != FS_PENDING) return;
+  if (row >= lc) return;
+  const double* dm = video + (int64_t)slot * vread_stride + (int64_t)CH_DEMOD * vchan_stride;
   const int W = C.outlinelen;
   uint16_t* out = pic + (int64_t)slot * pic_stride + (int64_t)row * W;
-  const double begin = lf[l], end = lf[l + 1];
   // ---- geometry (spline_block): y[j] = dm[ib + j], j = 0..n
   const int64_t ib = py_int(begin), ie = py_int(end);
   const int64_t n64 = ie - ib;
