@@ -71,6 +71,9 @@ extern "C" {
                            * store and its reload (another demod workgroup ran on the CU
                            * while this one was switched out: compute-wave save/restore
                            * on a shared GPU): its result is void, decode the read again */
+#define LDG_FS_VCUT 9     /* a field kernel needed the video channel past the read's video
+                           * cut (ldg_set_video_cut): its result is void, decode the read
+                           * again in full (ldg_decode_reads_async2, full[i] = 1)          */
 
 #define LDG_VBI_NONE (-2147483647 - 1) /* Python None in Field.vbi */
 
@@ -173,6 +176,16 @@ int ldg_decode_reads(ldg_ctx* ctx, int n, const int64_t* read_starts, const doub
  * can replay and output one batch while the next two decode. */
 int ldg_decode_reads_async(ldg_ctx* ctx, int n, const int64_t* read_starts, const double* mtf,
                            const int32_t* slots);
+/* The same with full[i] != 0 (full may be NULL) exempting read i from the video cut. */
+int ldg_decode_reads_async2(ldg_ctx* ctx, int n, const int64_t* read_starts, const double* mtf,
+                            const int32_t* slots, const uint8_t* full);
+/* Video cut (0, the default: none): the demod of later decodes stops each block whose
+ * outputs start at or past `out_samples` (read output index: sample start - 1024) after
+ * the sync channel -- the video, burst and pilot channels are not computed there.  A
+ * field whose lines reach past the cut comes back LDG_FS_VCUT: decode it again with
+ * full[i] = 1.  With a cut past the field (NTSC: ~10 lines before its vsync + 266
+ * lines), a read skips its tail blocks' video IFFT and stores. */
+int ldg_set_video_cut(ldg_ctx* ctx, int64_t out_samples);
 int ldg_decode_reads_wait(ldg_ctx* ctx, ldg_field_info* info);
 
 /* 48 kHz audio for fields in the given slots with the given starting time

@@ -41,6 +41,7 @@ enum FieldStatus {
   FS_CRASH = 6,           // reference would raise uncaught (e.g. vsync within first 11 peaks)
   FS_PENDING = 7,
   FS_MIGRATED = 8,        // the demod workgroup changed CU mid-block (its park was not private): decode again
+  FS_VCUT = 9,            // a field kernel needed a video sample past the read's video cut: decode again in full
 };
 
 // Per-read descriptor, written by the host before a batch.
@@ -54,6 +55,9 @@ struct ReadDesc {
   int32_t n_audio2;       // n_audio // 4
   int32_t filt_slot;      // index of the RF filter table (RFVideo * MTF**mtf)
   int32_t pad_;
+  int64_t vcut;           // demod outputs from here on need no video / burst / pilot channel
+                          // (blocks at or past it stop after the sync channel; a field kernel
+                          // that reaches past it flags FS_VCUT)
 };
 
 // System/filter scalars (lddecode_core.py:30-117, 119-279)

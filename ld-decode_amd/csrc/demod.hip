@@ -333,6 +333,7 @@ __device__ unsigned long long g_stamps[LDG_STAMP_BLOCKS][32];
   smap, reads, cap, cap_first, cap_nsamp, fmt, tw, twk, rf_filt, g_video, g_05, iir, a_lfilt, a_rfilt, C, video, \
       vread_stride, vchan_stride, audio1, aread_stride, achan_stride, status, ospill, stiles, aslice, sst, sbits, \
       bst, span
+template <bool CUT>
 __device__ __forceinline__ void demod_body(LDG_DEMOD_PARAMS) {
   __shared__ double2 s_x[M];          // 128 KiB: the 8192-point transforms
   __shared__ uint16_t s_bits[BLOCKLEN / 16];   // sync detector bits
@@ -649,6 +650,12 @@ __device__ __forceinline__ void demod_body(LDG_DEMOD_PARAMS) {
     }
   }
   STAMP(15);
+  // past the read's video cut nothing reads the video, burst or pilot channel (the
+  // field kernels check, FS_VCUT): the block ends after the sync channel
+  if (CUT && (int64_t)off >= rd.vcut) {
+    if (span && tid == 0) atomicMax(&span[1], (unsigned long long)__builtin_amdgcn_s_memrealtime());
+    return;
+  }
   double4 mlb, mtb, m15b, m31b;
   {
     if (!(kProbe & 32)) merge_pairs(X_, twk, g_video, tid, D);
@@ -707,13 +714,14 @@ __device__ __forceinline__ void demod_body(LDG_DEMOD_PARAMS) {
   if (span && tid == 0) atomicMax(&span[1], (unsigned long long)__builtin_amdgcn_s_memrealtime());
 }
 
-extern "C" __global__ __launch_bounds__(1024) void ldg_k_demod(LDG_DEMOD_PARAMS) { demod_body(LDG_DEMOD_ARGS); }
+extern "C" __global__ __launch_bounds__(1024) void ldg_k_demod(LDG_DEMOD_PARAMS) { demod_body<true>(LDG_DEMOD_ARGS); }
 
 // The same kernel under its own name for the benchmark's isolated roofline leg
 // (ldg_demod_isolated): its dispatches run alone on the GPU, so a kernel trace's
 // per-dispatch average of this symbol is the figure bench.py measures with HIP
-// events, undisturbed by the field kernels that co-run with ldg_k_demod.
-extern "C" __global__ __launch_bounds__(1024) void ldg_k_demod_iso(LDG_DEMOD_PARAMS) { demod_body(LDG_DEMOD_ARGS); }
+// events, undisturbed by the field kernels that co-run with ldg_k_demod.  It
+// demodulates every block in full (no video cut): the leg times whole reads.
+extern "C" __global__ __launch_bounds__(1024) void ldg_k_demod_iso(LDG_DEMOD_PARAMS) { demod_body<false>(LDG_DEMOD_ARGS); }
 
 // ---------------------------------------------------------------------------
 // Audio phase 1 (lddecode_core.py:321-328): per overlap-save block, the two

@@ -863,7 +863,7 @@ extern "C" __global__ __launch_bounds__(256) void ldg_k_hsync_field(const int32_
 // the previous crossing's bit sample, so a crossing costs ~one memory latency.
 extern "C" __global__ __launch_bounds__(192) void ldg_k_philips(
     const int32_t* __restrict__ smap, const double* __restrict__ video, int64_t vread_stride, int64_t vchan_stride, SysConst C,
-    FieldRec* __restrict__ recs, const double* __restrict__ lines) {
+    FieldRec* __restrict__ recs, const double* __restrict__ lines, const ReadDesc* __restrict__ reads) {
   prio_latency();
   __shared__ int32_t s_code[3][6];
   __shared__ int32_t s_ok[3];
@@ -876,6 +876,16 @@ extern "C" __global__ __launch_bounds__(192) void ldg_k_philips(
   const double* L2 = lines + (int64_t)slot * LINES_STRIDE + LL2 * MAX_LINES;
   const double fr = C.freq;
   const double thr = C.ire0 + (C.hz_ire * 50);
+  {
+    // the three code lines' searches stay within ~60 us of their line starts; past the
+    // read's video cut the read is decoded in full (uniform over the workgroup)
+    double hi = 0.0;
+    for (int q = 0; q < 3; q++) hi = fmax(hi, L2[C.codelines[q]]);
+    if (!(hi + 80 * fr < (double)reads[slot].vcut)) {
+      if (tid == 0) R->status = FS_VCUT;
+      return;
+    }
+  }
   {
     int ok = 0;
     const int ln = C.codelines[w];

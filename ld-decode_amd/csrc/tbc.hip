@@ -294,7 +294,7 @@ __device__ inline int calczc_s(const double* d, int len, int s, double target, i
 extern "C" __global__ __launch_bounds__(64) void ldg_k_burst_lines(
     const int32_t* __restrict__ smap, const double* __restrict__ video, int64_t vread_stride, int64_t vchan_stride, SysConst C,
     FieldRec* __restrict__ recs, double* __restrict__ lines, float* __restrict__ blevel, int pass,
-    const double4* __restrict__ bst) {
+    const double4* __restrict__ bst, const ReadDesc* __restrict__ reads) {
   prio_latency();
 
   // window rows for 40 outputs: <= 40 * SPL_MAXN / W + 2 * KTR + 4 < 384
@@ -317,6 +317,10 @@ extern "C" __global__ __launch_bounds__(64) void ldg_k_burst_lines(
   if (l >= nl) return;
   if (l >= lc) {
     if (lane == 0) { pv0[l] = 0.0; pv1[l] = 0.0; lvl[l] = 0.0f; }
+    return;
+  }
+  if (py_int(b1) + 1 >= reads[slot].vcut) {   // the window reaches past the read's video cut
+    if (lane == 0) R->status = FS_VCUT;
     return;
   }
   // demod_burst from the demod channel and the demod's per-chunk states (chan.hpp)
@@ -552,7 +556,7 @@ template <bool HOIST>
 __device__ __forceinline__ void final_lines_impl(
     const int32_t* __restrict__ smap, const double* __restrict__ video, int64_t vread_stride, int64_t vchan_stride,
     SysConst C, FieldRec* __restrict__ recs, const double* __restrict__ lines, const float* __restrict__ blevel,
-    uint16_t* __restrict__ pic, int64_t pic_stride) {
+    uint16_t* __restrict__ pic, int64_t pic_stride, const ReadDesc* __restrict__ reads) {
   prio_latency();
   __shared__ union {
     FinalLDS S;
@@ -582,6 +586,10 @@ __device__ __forceinline__ void final_lines_impl(
   const int64_t n64 = ie - ib;
   if (ib < 0 || n64 < 6 || n64 >= SPL_HARDN || ib + n64 + 1 > len) {
     if (tid == 0) R->status = FS_TBC;
+    return;
+  }
+  if (ib + n64 + 1 >= reads[slot].vcut) {     // samples past the read's video cut: decode it in full
+    if (tid == 0) R->status = FS_VCUT;
     return;
   }
   const bool pal = C.system == 1;
@@ -762,14 +770,14 @@ __device__ __forceinline__ void final_lines_impl(
 extern "C" __global__ __launch_bounds__(FINAL_NT, LDG_FINAL_WAVES) void ldg_k_final_lines(
     const int32_t* __restrict__ smap, const double* __restrict__ video, int64_t vread_stride, int64_t vchan_stride,
     SysConst C, FieldRec* __restrict__ recs, const double* __restrict__ lines, const float* __restrict__ blevel,
-    uint16_t* __restrict__ pic, int64_t pic_stride) {
-  final_lines_impl<false>(smap, video, vread_stride, vchan_stride, C, recs, lines, blevel, pic, pic_stride);
+    uint16_t* __restrict__ pic, int64_t pic_stride, const ReadDesc* __restrict__ reads) {
+  final_lines_impl<false>(smap, video, vread_stride, vchan_stride, C, recs, lines, blevel, pic, pic_stride, reads);
 }
 extern "C" __global__ __launch_bounds__(FINAL_NT, 5) void ldg_k_final_lines_h(
     const int32_t* __restrict__ smap, const double* __restrict__ video, int64_t vread_stride, int64_t vchan_stride,
     SysConst C, FieldRec* __restrict__ recs, const double* __restrict__ lines, const float* __restrict__ blevel,
-    uint16_t* __restrict__ pic, int64_t pic_stride) {
-  final_lines_impl<true>(smap, video, vread_stride, vchan_stride, C, recs, lines, blevel, pic, pic_stride);
+    uint16_t* __restrict__ pic, int64_t pic_stride, const ReadDesc* __restrict__ reads) {
+  final_lines_impl<true>(smap, video, vread_stride, vchan_stride, C, recs, lines, blevel, pic, pic_stride, reads);
 }
 
 // Mark reads still pending after the whole chain as valid.
@@ -883,7 +891,8 @@ extern "C" __global__ __launch_bounds__(64) void ldg_k_pilot_lines(const int32_t
                                                                    int64_t vread_stride, int64_t vchan_stride,
                                                                    SysConst C, FieldRec* __restrict__ recs,
                                                                    double* __restrict__ lines,
-                                                                   double* __restrict__ scratch) {
+                                                                   double* __restrict__ scratch,
+                                                                   const ReadDesc* __restrict__ reads) {
   prio_latency();
 
   constexpr int PW = 256;                       // 4.7 us at 40 MSPS: 188 samples
@@ -908,6 +917,10 @@ extern "C" __global__ __launch_bounds__(64) void ldg_k_pilot_lines(const int32_t
   py_slice(py_int(ll[l] - 4.7 * C.freq), py_int(ll[l]), len, a, b);
   const int pn = (int)(b > a ? b - a : 0);
   const int pm = pn < PW ? pn : PW;             // pn <= PW at the reference's sample rates
+  if (pn > 0 && b - 1 >= reads[slot].vcut) {    // past the read's video cut: decode it in full
+    if (lane == 0) R->status = FS_VCUT;
+    return;
+  }
   const double* d05 = video + (int64_t)slot * vread_stride + (int64_t)CH_05 * vchan_stride;
   for (int q = lane; q < pm; q += 64) s_pil[q] = dm[b - 1 - q] - d05[b - 1 - q];   // np.flip
   __syncthreads();

@@ -217,6 +217,16 @@ class GPUDecoder:
         self.miss_drain = os.environ.get('LDG_MISS_DRAIN', '1') == '1'
         self.grid_votes = int(os.environ.get('LDG_GRID_VOTES', '1'))   # _grid_next (1: the previous period's start)
         self.hist_len = max(16, self.grid_votes * P + 2)                  # valid field starts the planner keeps
+        # Video cut (ldg_set_video_cut): a steady-state read starts ~10 peaks before its
+        # field's vsync (lddecode_core.py:926, the previous field's nextfieldoffset), so its
+        # field ends ~276 NTSC / ~326 PAL lines into the read; the demod skips the video,
+        # burst and pilot channels of the read's blocks past the cut below (the last ~1/4
+        # of a 1,000,001-sample read).  A field that reaches past it (a capture's first
+        # read, a jump) comes back FS_VCUT and is decoded again in full.  LDG_VCUT=0: off.
+        vc = os.environ.get('LDG_VCUT')
+        self.video_cut = int(vc) if vc is not None else (740000 if self.sysp.name == 'NTSC' else 880000)
+        self.full_keys = set()
+        self.ctx.set_video_cut(self.video_cut)
         self.plan_located = 0              # leading fields the last plan walked on decoded reads
         self.htrace = [] if os.environ.get('LDG_HOSTTRACE') else None   # (perf_counter, event, n): host timeline
         self.comb, self.comb_sink = False, None
@@ -266,6 +276,7 @@ class GPUDecoder:
     def _reset_cache(self):
         self.cache, self.hints, self._hint_keys = {}, {}, []
         self.plan_located = 0
+        self.full_keys = set()             # reads that came back FS_VCUT (decoded again in full)
 
     # ---- forward simulator (plans the next GPU launch) ---------------------------
     def _next_known(self, start, info):
@@ -459,7 +470,8 @@ class GPUDecoder:
             raise RuntimeError('read cache full (capacity %d)' % self.capacity)
         slots = free[:len(keys)]
         t0 = time.perf_counter()
-        self.ctx.decode_reads_async([k[0] for k in keys], [k[1] for k in keys], slots)
+        full = [k in self.full_keys for k in keys] if self.full_keys else None
+        self.ctx.decode_reads_async([k[0] for k in keys], [k[1] for k in keys], slots, full)
         self.stats['gpu_s'] += time.perf_counter() - t0
         if self.htrace is not None:
             self.htrace.append((t0, 'launch', len(keys)))
@@ -488,6 +500,11 @@ class GPUDecoder:
                 # the demod's park was overwritten under it (compute-wave save/restore on a
                 # shared GPU): the read is void and stays undecoded; the replay's miss decodes it again
                 self.stats['migrated'] = self.stats.get('migrated', 0) + 1
+                continue
+            if inf.status == native.FS_VCUT:
+                # its field reaches past the video cut: void, and decoded again in full
+                self.stats['vcut_redo'] = self.stats.get('vcut_redo', 0) + 1
+                self.full_keys.add(k)
                 continue
             self.cache[k] = (sl, inf)
             if inf.status in (native.FS_VALID, native.FS_SHORT):

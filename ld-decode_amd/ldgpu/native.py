@@ -13,7 +13,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, 'libldgpu.so')
 
 LDG_OK = 0
-FS_VALID, FS_NO_VSYNC, FS_SHORT, FS_LINELOCS, FS_TBC, FS_EOF, FS_CRASH, FS_PENDING, FS_MIGRATED = range(9)
+FS_VALID, FS_NO_VSYNC, FS_SHORT, FS_LINELOCS, FS_TBC, FS_EOF, FS_CRASH, FS_PENDING, FS_MIGRATED, FS_VCUT = range(10)
 VBI_NONE = -2147483648
 LOG_NO_VSYNC = 1 << 16            # ldg_field_info.log_flags (include/ldgpu.h)
 MAX_VSYNCS = 16
@@ -23,7 +23,8 @@ EXPORTS = ['ldg_create', 'ldg_destroy', 'ldg_last_error', 'ldg_set_filters', 'ld
            'ldg_comb_ntsc', 'ldg_comb_reset', 'ldg_version', 'ldg_device_count', 'ldg_profile_enable',
            'ldg_profile_read', 'ldg_synth_capture', 'ldg_capture_download', 'ldg_comb_ntsc_async', 'ldg_sync', 'ldg_demod_isolated', 'ldg_comb_set_opts', 'ldg_output_async', 'ldg_output_wait',
            'ldg_host_alloc', 'ldg_host_free',
-           'ldg_archive_fields', 'ldg_archive_audio', 'ldg_decode_reads_async', 'ldg_decode_reads_wait',
+           'ldg_archive_fields', 'ldg_archive_audio', 'ldg_decode_reads_async', 'ldg_decode_reads_async2',
+           'ldg_set_video_cut', 'ldg_decode_reads_wait',
            'ldg_field_audio_async', 'ldg_field_audio_collect', 'ldg_comb_ntsc3d', 'ldg_cx_create', 'ldg_cx_destroy', 'ldg_cx_process', 'ldg_comb_pal', 'ldg_comb_set_state', 'ldg_profile_spans', 'ldg_profile_spans_union',
            'ldg_audio_offsets', 'ldg_comb_async']
 
@@ -124,6 +125,8 @@ def load(path=None):
     lib.ldg_comb_async.argtypes = [vp, C.c_int]
     lib.ldg_comb_ntsc3d.argtypes = [vp, C.c_int, vp, vp, C.POINTER(C.c_int), C.c_double, C.c_double]
     lib.ldg_decode_reads_async.argtypes = [vp, C.c_int, vp, vp, vp]
+    lib.ldg_decode_reads_async2.argtypes = [vp, C.c_int, vp, vp, vp, vp]
+    lib.ldg_set_video_cut.argtypes = [vp, C.c_int64]
     lib.ldg_decode_reads_wait.argtypes = [vp, vp]
     lib.ldg_archive_fields.argtypes = [vp, C.c_int, vp, C.c_int64]
     lib.ldg_archive_audio.argtypes = [vp, C.c_int, vp, vp, vp, C.c_int64, vp, vp]
@@ -286,14 +289,22 @@ class Context:
                 out[i] = x
         return out
 
-    def decode_reads_async(self, starts, mtfs, slots):
-        """Launch a decode (ldg_decode_reads_async, up to 4 outstanding); decode_reads_wait()
-        returns the records of the oldest outstanding one."""
+    def decode_reads_async(self, starts, mtfs, slots, full=None):
+        """Launch a decode (ldg_decode_reads_async2, up to 4 outstanding); decode_reads_wait()
+        returns the records of the oldest outstanding one.  full: per read, exempt it from the
+        video cut (set_video_cut; reads that came back FS_VCUT)."""
         s, m, sl = (np.ascontiguousarray(starts, dtype=np.int64), np.ascontiguousarray(mtfs, dtype=np.float64),
                     np.ascontiguousarray(slots, dtype=np.int32))
-        self._check(self.lib.ldg_decode_reads_async(self.h, s.size, s.ctypes.data, m.ctypes.data, sl.ctypes.data),
-                    'ldg_decode_reads_async')
+        f = None if full is None else np.ascontiguousarray(full, dtype=np.uint8)
+        self._check(self.lib.ldg_decode_reads_async2(self.h, s.size, s.ctypes.data, m.ctypes.data, sl.ctypes.data,
+                                                     None if f is None else f.ctypes.data),
+                    'ldg_decode_reads_async2')
         self._pending.append(s.size)
+
+    def set_video_cut(self, out_samples):
+        """The demod skips the video / burst / pilot channels of blocks whose outputs start at
+        or past out_samples (0: no cut); a field that needs them comes back FS_VCUT."""
+        self._check(self.lib.ldg_set_video_cut(self.h, int(out_samples)), 'ldg_set_video_cut')
 
     def decode_reads_wait(self):
         n = self._pending[0]

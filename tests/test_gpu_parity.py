@@ -233,6 +233,38 @@ def test_end_to_end_vs_golden(case, batch):
     print('%s batch=%d: %d/%d frames bit-identical' % (case, batch, exact, len(got)))
 
 
+@pytest.mark.parametrize('case', ['ntsc_clv_u8_0p2s', 'pal_clv_u8_0p2s', 'ntsc_cav_u8_mid_0p2s'])
+def test_video_cut_gives_the_same_decode(case, monkeypatch):
+    """The demod skips the video / burst / pilot channels of a read's blocks past its video
+    cut (ldg_set_video_cut); a field kernel reaching past it returns FS_VCUT and the read is
+    decoded again in full.  No cut, the default cut and a cut inside every field (every
+    read redone) must give the same frames, audio and metadata bit for bit."""
+    from ldgpu.decoder import GPUDecoder
+    from ldgpu.formats import NAME_TO_FMT
+    data, gold, frames, pcm, meta = oracle_decode(case)
+    c = gold['settings']
+    outs, redos = [], []
+    for cut in ('0', None, '200000'):
+        if cut is None:
+            monkeypatch.delenv('LDG_VCUT', raising=False)
+        else:
+            monkeypatch.setenv('LDG_VCUT', cut)
+        dec = GPUDecoder(system=c['system'], batch=8)
+        dec.set_capture(data, NAME_TO_FMT[c['fmt']])
+        got = []
+        dec.decode(sink=lambda fr, au, m: got.append((fr.copy(), au.copy(), m)))
+        outs.append(got)
+        redos.append(dec.stats.get('vcut_redo', 0))
+        dec.ctx.close()
+    assert redos[0] == 0 and redos[2] > 0, redos
+    for other in outs[1:]:
+        assert len(other) == len(outs[0])
+        for (f0, a0, m0), (f1, a1, m1) in zip(outs[0], other):
+            assert m0 == m1
+            assert np.array_equal(f0, f1)
+            assert np.array_equal(a0, a1)
+
+
 def test_end_to_end_pixels_vs_oracle(cav_capture):
     """Frame pixels within +-1 LSB and audio within +-1 of a fresh oracle decode."""
     mg, data = cav_capture

@@ -64,7 +64,10 @@ class FakeCtx:
     def set_filters(self, *a):
         pass
 
-    def decode_reads_async(self, starts, mtfs, slots):
+    def set_video_cut(self, out_samples):
+        pass
+
+    def decode_reads_async(self, starts, mtfs, slots, full=None):
         assert len(set(slots)) == len(slots) and all(0 <= s < self.max_reads for s in slots)
         busy = {s for p in self._pending for s in p[0]}
         assert not busy.intersection(slots), 'slot reused while in flight'
