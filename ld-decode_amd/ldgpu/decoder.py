@@ -236,6 +236,14 @@ class GPUDecoder:
         self.transitions = []              # audio-offset chain: linecount of each transition's field
         self.archive, self.arch_next, self.shard_frames = False, 0, []
         self._out_pending = None           # (frames, pics, audio fields, sink) awaiting their audio
+        # A flushed batch whose audio launch and the previous batch's collection (the
+        # host's one blocking wait besides the records) are deferred until the next
+        # decode launch is issued (_finish_flush): otherwise that wait, which ends only
+        # when the running demod leaves CUs to the audio kernels, sits between the
+        # replay and the next launch, and the demod queue runs dry for ~1 ms per batch.
+        self.defer_flush = os.environ.get('LDG_DEFER_FLUSH', '1') == '1'
+        self._staged = None
+        self._staged_slots = set()         # slots the staged batch still reads (never evicted)
         self.frame_log = None              # callback(lines): the reference's stdout lines of each frame
         self._obufs = None                 # pinned host rings for the asynchronous output path
         self._oring = 0
@@ -461,7 +469,8 @@ class GPUDecoder:
             used.update(sl)
         free = [s for s in range(self.capacity) if s not in used]
         if len(free) < len(keys):
-            for k in [k for k in self.cache if k not in protect][:len(keys) - len(free)]:
+            ss = self._staged_slots
+            for k in [k for k in self.cache if k not in protect and self.cache[k][0] not in ss][:len(keys) - len(free)]:
                 free.append(self.cache.pop(k)[0])      # oldest first (insertion / touch order)
             keys = keys[:len(free)]
         if not keys:
@@ -767,9 +776,11 @@ class GPUDecoder:
                 while self.pending:             # no launch outlives the call (an exception included)
                     self._launch_wait()
                 try:
+                    self._finish_flush()
                     self._emit_pending()
                 finally:
                     self._out_pending = None
+                    self._staged, self._staged_slots = None, set()
                     self.ctx.sync()
                     for ring in self._obufs or ():
                         for b in ring:
@@ -826,6 +837,7 @@ class GPUDecoder:
                 if not plan or not self._launch_async(plan, set(chain)):
                     break
                 launched += 1
+            self._finish_flush()
             frames = []
             eof = False
             missed = None
@@ -945,9 +957,23 @@ class GPUDecoder:
             af = []
         # the audio runs while the host plans and replays the next batch: this batch's
         # frames go to the sink at the next flush (or at the end of the decode)
+        self._staged = (frames, pics, af, sink)
+        if self.defer_flush:
+            self._staged_slots = set(tops) | set(bots) | {x.slot for _, x in af}
+        else:
+            self._finish_flush()
+
+    def _finish_flush(self):
+        """Hand the previous batch to the sink (waiting for its audio and output) and
+        launch the staged batch's audio."""
+        if self._staged is None:
+            return
+        staged, self._staged = self._staged, None
         self._emit_pending()
+        af = staged[2]
         self.ctx.field_audio_async([x.slot for _, x in af], [x.audio_offset for _, x in af])
-        self._out_pending = (frames, pics, af, sink)
+        self._staged_slots = set()
+        self._out_pending = staged
 
     def _emit_pending(self):
         """Collect the outstanding batch's audio and hand its frames to the sink."""
