@@ -241,7 +241,7 @@ class GPUDecoder:
         # decode launch is issued (_finish_flush): otherwise that wait, which ends only
         # when the running demod leaves CUs to the audio kernels, sits between the
         # replay and the next launch, and the demod queue runs dry for ~1 ms per batch.
-        self.defer_flush = os.environ.get('LDG_DEFER_FLUSH', '1') == '1'
+        self.defer_flush = os.environ.get('LDG_DEFER_FLUSH', '0') == '1'   # level on NTSC, PAL -8% in one pair (r04_zc): off
         self._staged = None
         self._staged_slots = set()         # slots the staged batch still reads (never evicted)
         self.frame_log = None              # callback(lines): the reference's stdout lines of each frame
