@@ -195,7 +195,11 @@ class GPUDecoder:
         self.sysp = self.rf.system
         self.batch = batch
         # two launches in flight + the batch the host replays + the cached path
-        self.depth = int(os.environ.get('LDG_DEPTH', '3'))   # launches kept in flight (3 vs 2: +2% since the planner stops at the last frame)
+        # launches kept in flight (3 vs 2: +2% since the planner stops at the last frame).
+        # NTSC 4: 20-step A/B +0.9 / +1.3 / +1.5% over 3 (r04_ze), its read chain
+        # predicts exactly, so a deeper speculation costs no reads.  PAL 3: 4 was
+        # 3-7% slower (more reads in flight over its start-up wander)
+        self.depth = int(os.environ.get('LDG_DEPTH', '4' if self.sysp.name == 'NTSC' else '3'))
         if not 1 <= self.depth <= 4:
             raise ValueError('LDG_DEPTH must be 1..4')
         self.capacity = capacity or max((self.depth + 2) * batch, batch + 16)
