@@ -591,7 +591,7 @@ def main():
         'cpu_baseline': cpu,
         'checks': dict(checks, synth_s=round(wl.synth_s, 2), reads_decoded=dec.stats['reads'],
                        reads_used=dec.stats['reads_used'], batches=dec.stats['batches'],
-                       misses=dec.stats.get('misses', 0), drain_waits=dec.stats.get('drain_waits', 0),
+                       misses=dec.stats.get('misses', 0), drain_waits=dec.stats.get('drain_waits', 0), vcut_redo=dec.stats.get('vcut_redo', 0),
                        park_redo=dec.stats.get('migrated', 0),
                        host_s={k: round(dec.stats.get(k, 0.0), 4)
                                for k in ('plan_s', 'gpu_s', 'replay_s', 'flush_s', 'wait_s')},
