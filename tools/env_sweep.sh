@@ -7,6 +7,6 @@ for i in $(seq 1 $REPS); do
   for e in $SETS; do
     envs=(); [ "$e" != "-" ] && IFS=, read -ra envs <<< "$e"
     out=$(env "${envs[@]}" timeout -k 10 300 python bench.py "$@" 2>/dev/null | tail -1)
-    echo "$e $(python -c "import json,sys; d=json.loads(sys.argv[1]); print(d['value'], d['ms_per_step'], d['roofline']['avg_launch_ms'])" "$out")"
+    echo "$e $(python -c "import json,sys; d=json.loads(sys.argv[1]); c=d.get('checks', {}); print(d['value'], d['ms_per_step'], d['roofline']['avg_launch_ms'], c.get('reads_decoded'), c.get('vcut_redo'))" "$out")"
   done
 done
