@@ -461,8 +461,11 @@ def main():
     t0 = time.perf_counter()
     frames = 0
     consumed = 0
+    step_ms = []                               # per-step wall (each step's decode ends synchronised)
     for k in range(args.steps):
+        ts = time.perf_counter()
         nf, ns = wl.step()
+        step_ms.append(round((time.perf_counter() - ts) * 1e3, 2))
         frames += nf
         consumed += ns
         progress(rank, 'step %d done' % (k + 1))
@@ -591,7 +594,7 @@ def main():
         'cpu_baseline': cpu,
         'checks': dict(checks, synth_s=round(wl.synth_s, 2), reads_decoded=dec.stats['reads'],
                        reads_used=dec.stats['reads_used'], batches=dec.stats['batches'],
-                       misses=dec.stats.get('misses', 0), drain_waits=dec.stats.get('drain_waits', 0), vcut_redo=dec.stats.get('vcut_redo', 0),
+                       misses=dec.stats.get('misses', 0), drain_waits=dec.stats.get('drain_waits', 0), vcut_redo=dec.stats.get('vcut_redo', 0), step_ms=step_ms,
                        park_redo=dec.stats.get('migrated', 0),
                        host_s={k: round(dec.stats.get(k, 0.0), 4)
                                for k in ('plan_s', 'gpu_s', 'replay_s', 'flush_s', 'wait_s')},
