@@ -232,6 +232,12 @@ int ldg_assemble_frames(ldg_ctx* ctx, int n, const int32_t* top_slots, const int
  * Copies up to `cap` bytes to host `dst`; returns bytes copied (>= 0) or an error. */
 int64_t ldg_debug_read(ldg_ctx* ctx, int slot, int what, void* dst, int64_t cap);
 
+/* Parity access to the demod's RF filter for one MTF level: RFVideo * MTF**mtf
+ * (RFVideo alone at mtf == 0: demodblock skips the product, lddecode_core.py:290-293),
+ * as the kernel ldg_k_rf_table builds it for a decode call.  dst: 16384 complex
+ * values (re, im interleaved), natural bin order. */
+int ldg_debug_rf_table(ldg_ctx* ctx, double mtf, double* dst);
+
 /* 2D NTSC comb (comb-ntsc.cxx dim=2 defaults, comb-ntsc.cxx:834-892) on n
  * 910x525 .tbc frames, rgb48 744x480 out (the frames comb-ntsc writes to
  * stdout, :704-733, :894-938).  State (the burst-level EMA aburstlev,

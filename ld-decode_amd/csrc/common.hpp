@@ -11,6 +11,7 @@ constexpr int BLOCKCUT_END = 32;                      // F05_offset
 constexpr int BLOCKSTEP = BLOCKLEN - BLOCKCUT - BLOCKCUT_END;   // 15328
 constexpr int HALF = BLOCKLEN / 2;                     // 8192-point complex FFTs
 constexpr int MAX_BLOCKS_PER_READ = 66;
+constexpr int PARK_SLOTS = 2048;                       // demod odd-half parks: one per physical CU (demod.hip)
 constexpr int READLEN = 1000000;
 constexpr int MAX_NOUT = READLEN + 1026 + 16;          // end - start + 1 (+ slack)
 constexpr int AUDIO_DIV1 = 16;                         // 40 MHz -> 2.5 MHz (blocklen / 1024)

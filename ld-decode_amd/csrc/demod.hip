@@ -125,8 +125,7 @@ __device__ __forceinline__ Slot slot_of(int tid, int c) {
 }
 
 // This workgroup's physical CU: (XCC, SE, SH, CU) from HW_REG_XCC_ID / HW_REG_HW_ID
-// (gfx9 HW_ID: CU_ID [11:8], SH_ID [12], SE_ID [15:13]), < PARK_SLOTS.
-constexpr int PARK_SLOTS = 2048;
+// (gfx9 HW_ID: CU_ID [11:8], SH_ID [12], SE_ID [15:13]), < PARK_SLOTS (common.hpp).
 // One park per CU is private only while two demod workgroups can never share a CU
 // (also across the two demod streams' concurrent launches): the transform buffer
 // alone is more than half of the CU's 160 KiB of LDS.
@@ -180,11 +179,10 @@ __device__ __forceinline__ void st_pair(double* a, double2 z) {
 // The odd-half park's stores (read back by LDS-DMA on the same CU): plain
 // stores ("nt" measured +1.5%, "sc0" even).
 __device__ __forceinline__ void st_park(double2* a, double2 z) { *a = z; }
-// a parked value's signature (bit pattern of both parts; summed over a thread's stores)
-__device__ __forceinline__ uint32_t park_sig(double2 z) {
-  const uint64_t x = (uint64_t)__double_as_longlong(z.x), y = (uint64_t)__double_as_longlong(z.y);
-  const uint64_t v = x ^ ((y << 29) | (y >> 35));
-  return (uint32_t)v ^ (uint32_t)(v >> 32);
+// The park's owner words: PARK_SLOTS 64-bit words after the parks (ospill + PARK_SLOTS * M),
+// word u = the tag of the last workgroup that claimed park u (see demod_body).
+__device__ __forceinline__ unsigned long long* park_owner(double2* ospill) {
+  return reinterpret_cast<unsigned long long*>(ospill + (int64_t)PARK_SLOTS * M);
 }
 __device__ __forceinline__ void store_pair(double* o, int m, double2 z, int copylen) {
   const int p = 2 * m;
@@ -326,12 +324,14 @@ __device__ unsigned long long g_stamps[LDG_STAMP_BLOCKS][32];
       const double2 *__restrict__ g_05, const double *__restrict__ iir, const double2 *__restrict__ a_lfilt,      \
       const double2 *__restrict__ a_rfilt, SysConst C, double *__restrict__ video, int64_t vread_stride,          \
       int64_t vchan_stride, double *__restrict__ audio1, int64_t aread_stride, int64_t achan_stride,              \
-      int32_t *__restrict__ status, double2 *__restrict__ ospill, SyncTile *__restrict__ stiles,                 \
+      int32_t *__restrict__ status, double2 *__restrict__ ospill, unsigned long long park_epoch,                 \
+      SyncTile *__restrict__ stiles,                                                                             \
       double2 *__restrict__ aslice, double *__restrict__ sst, uint32_t *__restrict__ sbits,                      \
       double4 *__restrict__ bst, unsigned long long *__restrict__ span
 #define LDG_DEMOD_ARGS                                                                                            \
   smap, reads, cap, cap_first, cap_nsamp, fmt, tw, twk, rf_filt, g_video, g_05, iir, a_lfilt, a_rfilt, C, video, \
-      vread_stride, vchan_stride, audio1, aread_stride, achan_stride, status, ospill, stiles, aslice, sst, sbits, \
+      vread_stride, vchan_stride, audio1, aread_stride, achan_stride, status, ospill, park_epoch, stiles, aslice,  \
+      sst, sbits,                                                                                                 \
       bst, span
 template <bool CUT>
 __device__ __forceinline__ void demod_body(LDG_DEMOD_PARAMS) {
@@ -340,7 +340,6 @@ __device__ __forceinline__ void demod_body(LDG_DEMOD_PARAMS) {
   __shared__ double2 s_tw[TW_LDS_N];           // per-lane FFT twiddles (fft8k.hpp)
   __shared__ IIRAux s_aux;
   __shared__ double s_atan[65];
-  __shared__ uint32_t s_park_sig[1024];        // each thread's first park store's signature
   const CBuf X_{s_x};
   const int tid = threadIdx.x;
   if (tid < 65) s_atan[tid] = c_atan64[tid];   // ordered by the first transform's barrier
@@ -372,6 +371,12 @@ __device__ __forceinline__ void demod_body(LDG_DEMOD_PARAMS) {
   // stays cache-resident instead of streaming 1 GB per launch through HBM.
   const int my_cu = cu_slot();
   double2* park = ospill + (int64_t)my_cu * M;
+  // Claim the park before any store to it: its owner word takes this workgroup's tag
+  // (unique per launch and workgroup), made visible before the park stores (the
+  // fence below, ahead of the barrier that precedes them).  See the check at the reload.
+  unsigned long long* owner = park_owner(ospill) + my_cu;
+  const unsigned long long my_tag = (park_epoch << 32) | (unsigned long long)blockIdx.x;
+  if (tid == 0) __hip_atomic_store(owner, my_tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   constexpr double TAU = 6.283185307179586;
 
   // ---- 1. raw samples -> z[m] = x[2m] + i x[2m+1]; forward FFT ---------------
@@ -434,6 +439,8 @@ __device__ __forceinline__ void demod_body(LDG_DEMOD_PARAMS) {
       as[j] = al;
       as[1024 + j] = ar;
     }
+    // the claim (issued at the start, long complete) is visible before any park store
+    if (tid == 0) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     __syncthreads();
     const int t = fresh(tid);
 #pragma unroll
@@ -448,7 +455,6 @@ __device__ __forceinline__ void demod_body(LDG_DEMOD_PARAMS) {
       if (!(kProbe & 256)) {
         const double2 o = cmulc(csub(yk, yk2), wk);
         st_park(park + SW(sl.p), o);
-        if (c == 0) s_park_sig[tid] = park_sig(o);         // pair 0 is live on every thread
       }
       if (sl.pp != sl.p) {
         const double2 ykp = cmul(X.b[c], Fv(sl.pp));
@@ -471,25 +477,20 @@ __device__ __forceinline__ void demod_body(LDG_DEMOD_PARAMS) {
   for (int h = 0; h < 2; h++) {
     STAMP(4 + 2 * h);
 #ifndef LDG_NO_PARK_CHECK   // (timing probes only)
-    if (h == 1 && !(kProbe & (16 | 256))) {
-      // The park is private to this CU only while no other demod workgroup runs on
-      // it between this one's stores and its reload.  Compute-wave save/restore (a
-      // shared or oversubscribed GPU) can break that -- this workgroup switched
-      // out, another one parking on the CU, this one resumed on the same CU or
-      // another.  Each thread compares the signature of the first value it parked
-      // with the reloaded LDS image of that slot: a foreign workgroup's wave stores
-      // the same slots as this one's wave, in the same order, so any of its stores
-      // that landed before the reload includes that first slot of each of its
-      // threads (one that lands after the reload does not touch this block's data).
-      // A mismatch flags the read and the host decodes it again (FS_MIGRATED).
-      // (The round-3 form re-read the slot from the park in global memory: one
-      // memory latency per block.)  This is a HEURISTIC, not a proof: global stores
-      // to different addresses (different L2 channels) are not ordered, so a
-      // foreign wave's partial overwrite could land without its first slot and go
-      // undetected.  Migration needs compute-wave save/restore of a demod workgroup
-      // (a shared or oversubscribed GPU); every run so far reported 0 redos.
-      const double2 pv = s_x[SW(slot_of(fresh(tid), 0).p)];
-      if (park_sig(pv) != s_park_sig[tid]) status[slot] = FS_MIGRATED;
+    if (h == 1 && tid == 0 && !(kProbe & (16 | 256))) {
+      // The park is private to this CU only while no other demod workgroup stores to it
+      // between this one's stores and its reload (just completed: vmcnt(0) and the barrier
+      // above).  Compute-wave save/restore (a shared or oversubscribed GPU) can break that:
+      // this workgroup switched out, another one parking on the CU, this one resumed.  Every
+      // workgroup claims the park (owner word = its tag) and makes the claim visible before
+      // its first park store; so if any foreign store landed before this reload read it, the
+      // foreign claim landed before that, after this workgroup's own claim, and the owner
+      // word read now (device-coherent, after the reload completed) is no longer this
+      // workgroup's tag.  The check is exact: a mismatch flags the read (FS_MIGRATED) and
+      // the host decodes it again; a match proves the reloaded half is this block's own.
+      // (A foreign claim without data stores before the reload flags a read that was in
+      // fact intact: a redo, never a wrong result.)
+      if (__hip_atomic_load(owner, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != my_tag) status[slot] = FS_MIGRATED;
     }
 #endif
     double2 zr[8];

@@ -215,6 +215,43 @@ def load_window(dec, raw, fmt, rank, world, start, rccl, start_frame=0, length=N
     return buf
 
 
+def widen_window(dec, raw, fmt, rccl, sample, keep):
+    """A resumed decode (the last rank reading on past the decode's nominal end over
+    skipped fields) needs samples past its window: make [a frame before `sample`, eight
+    frames and a read after it) resident from storage.  keep: holds the buffer alive."""
+    import torch
+    from ldgpu.shard import sample_byte, widen_window as window_at
+    lo, hi = window_at(sample, dec.rf.samples_per_frame, dec.cap_nsamples)
+    nbytes = raw.size
+    bl, bh = sample_byte(fmt, lo), (nbytes if hi >= dec.cap_nsamples else sample_byte(fmt, hi))
+    src = torch.from_numpy(np.ascontiguousarray(raw[bl:bh]))
+    if rccl:
+        buf = src.to('cuda')
+        torch.cuda.synchronize()
+        dec.set_capture(None, fmt, device_ptr=buf.data_ptr(), nsamples=hi - lo, first_sample=lo, total_bytes=nbytes)
+    else:
+        buf = src
+        dec.set_capture(buf.numpy(), fmt, first_sample=lo, total_bytes=nbytes)
+    keep[:] = [buf]
+    print('capture window widened to samples [%d, %d)' % (lo, hi))
+
+
+def write_manifest(path, man):
+    """Replace the manifest atomically and durably: the temp file's bytes, the rename
+    and the directory entry reach storage before the next epoch starts."""
+    tmp = path + '.tmp'
+    with open(tmp, 'w') as fh:
+        json.dump(man, fh)
+        fh.flush()
+        os.fsync(fh.fileno())
+    os.replace(tmp, path)
+    d = os.open(os.path.dirname(os.path.abspath(path)), os.O_RDONLY)
+    try:
+        os.fsync(d)
+    finally:
+        os.close(d)
+
+
 def sharded(args, dec, outname, firstframe, num_frames, nextsample, req_frames, raw, fmt, rccl, world):
     """This rank's share of a field-group sharded decode (any world size), in epochs of
     --epoch-frames frames (default: one epoch).  Every rank writes its frames at their
@@ -247,28 +284,45 @@ def sharded(args, dec, outname, firstframe, num_frames, nextsample, req_frames, 
 
     exts = ('.tbc', '.pcm', '.rgb') if args.comb else ('.tbc', '.pcm')
     parts = outname + '.json.part'             # one JSON line of frame metadata per finished epoch
+    st = os.stat(args.infile)
+    # what makes the manifest this decode's: the input (path, size, mtime), the frame
+    # range and every option that changes the outputs or the chain state it carries
+    ident = {'infile': os.path.abspath(args.infile), 'infile_size': st.st_size, 'infile_mtime_ns': st.st_mtime_ns,
+             'exts': list(exts), 'num_frames': num_frames, 'firstframe': firstframe, 'seek': args.seek,
+             'start_sample': int(nextsample), 'system': dec.sysp.name, 'comb': bool(args.comb),
+             'comb_args': args.comb_args, 'no_json': bool(args.no_json)}
     man = None
     if args.manifest and os.path.exists(args.manifest):
         with open(args.manifest) as fh:
             man = json.load(fh)
-        if man.get('infile_size') != os.path.getsize(args.infile) or man.get('exts') != list(exts) or \
-                man.get('num_frames') != num_frames:
+        if any(man.get(k) != v for k, v in ident.items()):
             print('ERROR: %s belongs to another decode' % args.manifest)
             return 1
+        if man.get('complete'):
+            if rank == 0:
+                print('%s: the decode is already complete (%d frames)' % (args.manifest, man['frames']))
+            if world > 1:
+                import torch.distributed as dist
+                dist.destroy_process_group()
+            return 0
         if rank == 0:
             print('resuming after epoch %d (%d frames written)' % (man['epoch'], man['frames']))
     if man is None:
-        man = {'infile_size': os.path.getsize(args.infile), 'exts': list(exts), 'num_frames': num_frames,
-               'epoch': 0, 'frames': 0, 'pcm_bytes': 0, 'state': None, 'nextsample': int(nextsample),
-               'complete': False}
+        man = dict(ident, epoch=0, frames=0, pcm_bytes=0, state=None, nextsample=int(nextsample), complete=False)
         if rank == 0:
             for ext in exts:
                 open(outname + ext, 'wb').close()
             open(parts, 'w').close()
     elif rank == 0:
-        # drop a metadata line written after the manifest's last epoch (a crash in between)
-        with open(parts) as fh:
-            lines = fh.readlines()[:man['epoch']]
+        # drop a metadata line written after the manifest's last epoch (a crash in between);
+        # a part file lost with nothing in it yet (epoch 0) starts empty
+        lines = []
+        if os.path.exists(parts):
+            with open(parts) as fh:
+                lines = fh.readlines()[:man['epoch']]
+        elif man['epoch'] and not args.no_json:
+            print('ERROR: %s is missing; the metadata of the finished epochs is lost' % parts)
+            return 1
         with open(parts, 'w') as fh:
             fh.writelines(lines)
     barrier()
@@ -278,9 +332,11 @@ def sharded(args, dec, outname, firstframe, num_frames, nextsample, req_frames, 
     stats = {}
     while not man['complete'] and man['frames'] < num_frames:
         n = min(epoch_frames, num_frames - man['frames'])
-        keep = None
+        keep = []
+        widen = None
         if world > 1:
-            keep = load_window(dec, raw, fmt, rank, world, man['nextsample'], rccl, firstframe, n)   # noqa: F841
+            keep = [load_window(dec, raw, fmt, rank, world, man['nextsample'], rccl, firstframe, n)]
+            widen = lambda s, keep=keep: widen_window(dec, raw, fmt, rccl, s, keep)   # noqa: E731
         ep = {}
         # the rank's frames (and with --comb their rgb48, combed in HBM as they are decoded)
         # wait in spill files beside the outputs until their global offsets are known
@@ -288,7 +344,7 @@ def sharded(args, dec, outname, firstframe, num_frames, nextsample, req_frames, 
         res = decode_sharded(dec, rank, world, allgather, start_frame=firstframe, length=n,
                              start_sample=man['nextsample'], whole_capture=whole,
                              spill_dir=os.path.dirname(os.path.abspath(outname)), comb=args.comb, stats=stats,
-                             init=man['state'], epoch_end=ep)
+                             init=man['state'], epoch_end=ep, widen=widen)
         sizes = allgather((len(res), sum(r[2].nbytes for r in res)))
         first = man['frames'] + sum(k for k, _ in sizes[:rank])
         pcm_off = man['pcm_bytes'] + sum(b for _, b in sizes[:rank])
@@ -299,6 +355,9 @@ def sharded(args, dec, outname, firstframe, num_frames, nextsample, req_frames, 
                 print('frame ', r[3]['vbi']['framenr'])
                 tbc.write(r[1].tobytes())
                 pcm.write(r[2].tobytes())
+            for fh in (tbc, pcm):         # on storage before the manifest claims the epoch
+                fh.flush()
+                os.fsync(fh.fileno())
         if args.comb:
             # combed in HBM during the decode; the burst-level EMA (comb-ntsc.cxx:560-566,
             # global over every frame) was handed across the ranks and the first frames
@@ -309,6 +368,8 @@ def sharded(args, dec, outname, firstframe, num_frames, nextsample, req_frames, 
                 fh.seek(first * rgb_bytes)
                 for r in res:
                     fh.write(np.ascontiguousarray(r[4]).tobytes())
+                fh.flush()
+                os.fsync(fh.fileno())
         metas = allgather([r[3] for r in res])
         total = sum(k for k, _ in sizes)
         barrier()                                    # every rank's bytes of this epoch are written
@@ -325,10 +386,7 @@ def sharded(args, dec, outname, firstframe, num_frames, nextsample, req_frames, 
                 fh.flush()
                 os.fsync(fh.fileno())
             if args.manifest:
-                tmp = args.manifest + '.tmp'
-                with open(tmp, 'w') as fh:
-                    json.dump(man, fh)
-                os.replace(tmp, args.manifest)
+                write_manifest(args.manifest, man)
         barrier()
         if int(os.environ.get('LDG_FAULT_AFTER_EPOCHS', '0') or 0) == man['epoch']:
             print('rank %d: fault injected after epoch %d (LDG_FAULT_AFTER_EPOCHS)' % (rank, man['epoch']), flush=True)
@@ -341,12 +399,11 @@ def sharded(args, dec, outname, firstframe, num_frames, nextsample, req_frames, 
                 allm = [m for line in fh for m in json.loads(line)]
             with open(outname + '.json', 'w') as fh:
                 json.dump(allm, fh)
-        os.remove(parts)
         if args.manifest:
+            # complete before the part file goes: a rerun then finds the decode done
             man['complete'] = True
-            with open(args.manifest + '.tmp', 'w') as fh:
-                json.dump(man, fh)
-            os.replace(args.manifest + '.tmp', args.manifest)
+            write_manifest(args.manifest, man)
+        os.remove(parts)
     barrier()
     if world > 1:
         import torch.distributed as dist

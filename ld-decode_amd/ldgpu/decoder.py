@@ -45,7 +45,14 @@ class ReferenceCrash(RuntimeError):
 
 
 class WindowMiss(RuntimeError):
-    """A read needs capture samples outside the resident window (sharded decode)."""
+    """A read needs capture samples outside the resident window (sharded decode).
+    Raised by decode() after every frame before the one that needed the read was
+    emitted, with the framer restored to that frame's start: resume_at is its start
+    sample, so a resumed decode (resume=True) from there continues exactly."""
+
+    def __init__(self, msg, resume_at=None):
+        super().__init__(msg)
+        self.resume_at = resume_at
 
 
 def read_geometry(start):
@@ -855,6 +862,7 @@ class GPUDecoder:
             frames = []
             eof = False
             missed = None
+            window_miss = None
             t0 = time.perf_counter()
             self.requested = []
             while done + len(frames) < num_frames and self._tell() + bpf * 1.05 <= size and more(nextsample):
@@ -869,6 +877,14 @@ class GPUDecoder:
                     (nextsample, self.mtf_level, self.audio_offset, self.last_framenr, self.last_isclv,
                      self.last_read, nt, nframes_read) = cp
                     del self.transitions[nt:]
+                    break
+                except WindowMiss as wm:
+                    # no launch can fix this one: back to the frame's checkpoint, emit the
+                    # frames before it, then raise with the resume point
+                    (nextsample, self.mtf_level, self.audio_offset, self.last_framenr, self.last_isclv,
+                     self.last_read, nt, nframes_read) = cp
+                    del self.transitions[nt:]
+                    window_miss = WindowMiss(str(wm), resume_at=int(nextsample))
                     break
                 if fr is None:
                     eof = True
@@ -902,6 +918,8 @@ class GPUDecoder:
                 self.htrace.append((time.perf_counter(), 'flushed', len(frames)))
             done += len(frames)
             self.stats['reads_used'] += sum(len(f.fields) for f in frames)
+            if window_miss is not None:
+                raise window_miss
             if eof or (not frames and not launched and not self.pending):
                 break
             self._launch_wait()                 # the oldest launch: the replay continues into it

@@ -26,7 +26,7 @@ EXPORTS = ['ldg_create', 'ldg_destroy', 'ldg_last_error', 'ldg_set_filters', 'ld
            'ldg_archive_fields', 'ldg_archive_audio', 'ldg_decode_reads_async', 'ldg_decode_reads_async2',
            'ldg_set_video_cut', 'ldg_decode_reads_wait',
            'ldg_field_audio_async', 'ldg_field_audio_collect', 'ldg_comb_ntsc3d', 'ldg_cx_create', 'ldg_cx_destroy', 'ldg_cx_process', 'ldg_comb_pal', 'ldg_comb_set_state', 'ldg_profile_spans', 'ldg_profile_spans_union',
-           'ldg_audio_offsets', 'ldg_comb_async']
+           'ldg_audio_offsets', 'ldg_comb_async', 'ldg_debug_rf_table']
 
 
 class FieldInfo(C.Structure):
@@ -114,6 +114,7 @@ def load(path=None):
                                         C.POINTER(C.c_uint16), C.c_int]
     lib.ldg_debug_read.argtypes = [vp, C.c_int, C.c_int, vp, C.c_int64]
     lib.ldg_debug_read.restype = C.c_int64
+    lib.ldg_debug_rf_table.argtypes = [vp, C.c_double, vp]
     lib.ldg_comb_ntsc.argtypes = [vp, C.c_int, vp, vp, C.c_int]
     lib.ldg_comb_reset.argtypes = [vp]
     lib.ldg_comb_set_opts.argtypes = [vp, C.POINTER(CombOpts)]
@@ -383,6 +384,14 @@ class Context:
         if rc < 0:
             raise LDGError('ldg_debug_read(%d,%d) -> %d' % (slot, what, rc))
         return a[:rc // a.itemsize]
+
+    def rf_table(self, mtf):
+        """The demod's RF filter RFVideo * MTF**mtf (complex128[16384], natural bin order)."""
+        a = np.zeros(2 * 16384, dtype=np.float64)
+        rc = self.lib.ldg_debug_rf_table(self.h, float(mtf), a.ctypes.data_as(C.c_void_p))
+        if rc != LDG_OK:
+            raise LDGError('ldg_debug_rf_table(%r) -> %d' % (mtf, rc))
+        return a.view(np.complex128)
 
     def comb_ntsc(self, frames):
         """2D NTSC comb (comb-ntsc.cxx dim=2): n x (525, 910) uint16 frames -> n x (480, 744, 3) rgb48

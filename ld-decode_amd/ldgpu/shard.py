@@ -56,19 +56,28 @@ def sample_byte(fmt, s):
 
 def shard_windows(bounds, spf, nsamples, warmup_frames=2, halo_frames=2):
     """Per rank (lo, cut, hi): the resident samples [lo, hi), read from storage
-    [lo, cut) and received from the next rank [cut, hi)."""
+    [lo, cut) and received from the next rank [cut, hi).  The last rank's window ends
+    like the others' past the decode's end (bounds[-1], the frame limit's reach), not at
+    the end of the capture: an epoch of a long capture keeps O(epoch) samples resident.
+    Reads past it (the last rank extending over skipped fields, ShardedDecode.extend)
+    widen the window (ShardedDecode widen)."""
     world = len(bounds) - 1
     out = []
     for k in range(world):
         first = bounds[k] - (warmup_frames * spf if k else 0)
         lo = max(0, (first - 1024) // GROUP * GROUP)
-        if k == world - 1:
-            cut = hi = nsamples
-        else:
-            cut = bounds[k + 1] // GROUP * GROUP
-            hi = min(nsamples, -(-(bounds[k + 1] + halo_frames * spf + READ_SPAN) // GROUP) * GROUP)
+        hi = min(nsamples, -(-(bounds[k + 1] + halo_frames * spf + READ_SPAN) // GROUP) * GROUP)
+        cut = hi if k == world - 1 else bounds[k + 1] // GROUP * GROUP
         out.append((lo, cut, hi))
     return out
+
+
+def widen_window(sample, spf, nsamples, ahead_frames=8):
+    """The window a rank reloads when a resumed decode reads past its window at `sample`
+    (WindowMiss.resume_at): from a frame before it to `ahead_frames` frames and a read past it."""
+    lo = max(0, (sample - spf - 1024) // GROUP * GROUP)
+    hi = min(nsamples, -(-(sample + ahead_frames * spf + READ_SPAN) // GROUP) * GROUP)
+    return lo, hi
 
 
 def halo_plan(windows):
@@ -262,9 +271,11 @@ class ShardedDecode:
     """One rank's part of a field-group sharded decode, in two phases."""
 
     def __init__(self, dec, rank, world, start_frame=0, warmup_frames=2, length=None, start_sample=None,
-                 whole_capture=None, spill_dir=None, resident=False, comb=False, init=None):
+                 whole_capture=None, spill_dir=None, resident=False, comb=False, init=None, widen=None):
         """whole_capture: callable that makes the whole capture resident (the fallback
-        when a capture window turns out too small).  spill_dir: where the output
+        when a capture window turns out too small).  widen: callable(sample) that makes
+        a window around `sample` resident (widen_window): a resumed decode (the last
+        rank's extension) that reads past its window continues there instead.  spill_dir: where the output
         frames wait for the exchange (FrameSpill; default: the system temp dir).
         resident: the frames stay in HBM (benchmark mode: decode(sink=None), the fused
         comb with comb=True); nothing is spilled.
@@ -275,6 +286,7 @@ class ShardedDecode:
         self.init = init
         self.resident, self.comb = resident, comb
         self.whole_capture, self.window_misses, self.extended = whole_capture, 0, 0
+        self.widen, self.widened = widen, 0
         self.spf = dec.rf.samples_per_frame
         # the whole decode's frame count limit (lddecode.py:49; -l): frames past it are dropped
         self.bounds, self.limit, self.start = decode_bounds(dec.cap_nsamples, dec.cap_bytes, self.spf, world,
@@ -303,6 +315,26 @@ class ShardedDecode:
             if sink:
                 sink(pic, None, meta)
 
+        if resume:
+            # continue the decode this rank holds; a read past the window (the decoder
+            # stopped at the checkpoint of the frame that needed it, every earlier frame
+            # emitted) widens the window and the decode goes on from that frame
+            n0 = len(dec.shard_frames)
+            while True:
+                left = None if length is None else length - (len(dec.shard_frames) - n0)
+                try:
+                    dec.decode(start_sample=start_sample, stop_sample=stop, keep_from=keep_from, firstframe=firstframe,
+                               archive=True, sink=None if self.resident else keep, init_state=init,
+                               comb=self.comb, length=left, resume=True,
+                               comb_sink=self.rgb.append if self.rgb is not None else None)
+                    return
+                except WindowMiss as e:
+                    if self.widen is None or e.resume_at is None:
+                        raise
+                    self.widen(e.resume_at)
+                    self.widened += 1
+                    start_sample, init = e.resume_at, None
+
         for attempt in range(2):
             if not resume:
                 self.frames.reset()
@@ -316,9 +348,7 @@ class ShardedDecode:
                 return
             except WindowMiss:
                 # a read outside this rank's capture window: decode from the whole capture
-                # (not for a resumed decode: only the last rank resumes, and its window
-                # runs to the end of the capture)
-                if attempt or self.whole_capture is None or resume:
+                if attempt or self.whole_capture is None:
                     raise
                 self.whole_capture()
                 self.window_misses += 1
@@ -475,7 +505,7 @@ def comb_fix(sd, allgather, nkept, stats=None):
 
 def decode_sharded(dec, rank, world, allgather, sink=None, start_frame=0, length=None, start_sample=None,
                    whole_capture=None, spill_dir=None, resident=False, comb=False, stats=None, init=None,
-                   epoch_end=None):
+                   epoch_end=None, widen=None):
     """Run all phases with `allgather(obj) -> [obj per rank]` (torch.distributed
     all_gather_object, or an in-process stand-in).  Returns this rank's
     [(global_index, frame, pcm, meta)] (with comb: [(..., meta, rgb48)], the exact
@@ -493,18 +523,19 @@ def decode_sharded(dec, rank, world, allgather, sink=None, start_frame=0, length
     gc.disable()
     try:
         return _decode_sharded(dec, rank, world, allgather, sink, start_frame, length, start_sample,
-                               whole_capture, spill_dir, resident, comb, stats, init, epoch_end)
+                               whole_capture, spill_dir, resident, comb, stats, init, epoch_end, widen)
     finally:
         if gc_on:
             gc.enable()
 
 
 def _decode_sharded(dec, rank, world, allgather, sink, start_frame, length, start_sample, whole_capture,
-                    spill_dir, resident, comb, stats, init, epoch_end):
+                    spill_dir, resident, comb, stats, init, epoch_end, widen):
     import time
     t0 = time.perf_counter()
     sd = ShardedDecode(dec, rank, world, start_frame, length=length, start_sample=start_sample,
-                       whole_capture=whole_capture, spill_dir=spill_dir, resident=resident, comb=comb, init=init)
+                       whole_capture=whole_capture, spill_dir=spill_dir, resident=resident, comb=comb, init=init,
+                       widen=widen)
     loc = sd.local()
     t1 = time.perf_counter()
     summ = allgather(loc)
@@ -536,6 +567,7 @@ def _decode_sharded(dec, rank, world, allgather, sink, start_frame, length, star
             stats[k] = stats.get(k, 0.0) + v
         stats['refixes'] = stats.get('refixes', 0) + refixes
         stats['window_misses'] = stats.get('window_misses', 0) + sd.window_misses
+        stats['window_widened'] = stats.get('window_widened', 0) + sd.widened
         stats['extended_frames'] = stats.get('extended_frames', 0) + sd.extended
         stats['frames_total'] = sum(s['n'] for s in summ)
     if resident:

@@ -38,6 +38,15 @@ CASES = {
     # a capture that starts 300,000 samples into a field (the first read's short
     # nextfieldoffset, demod's start-1024 quirk at the file start, lddecode_core.py:378-380)
     'ntsc_cav_u8_mid_0p2s': dict(seconds=0.2, fmt='u8', system='NTSC', kw={'seed': 10}, skip=300000),
+    # the MTF chain away from MTF ~ 1 (Framer.readframe, lddecode_core.py:1300-1309; demodblock
+    # :292-293): a CAV capture from picture ~1200, whose first frame is decoded at MTF 1, then
+    # dropped and the next one re-read at MTF 0.88 ...
+    'ntsc_cav_u8_mtf_0p3s': dict(seconds=0.3, fmt='u8', system='NTSC', kw={'seed': 11, 'first_frame': 1200}),
+    # ... one crossing picture 9999 -> 10001, where the MTF clamps to 0 and demodblock skips
+    # the MTF product (mtf_level == 0) ...
+    'ntsc_cav_u8_mtf0_0p3s': dict(seconds=0.3, fmt='u8', system='NTSC', kw={'seed': 12, 'first_frame': 9997}),
+    # ... and a PAL CAV disc from picture ~1200 (the same chain on FieldPAL)
+    'pal_cav_u8_mtf_0p3s': dict(seconds=0.3, fmt='u8', system='PAL', kw={'seed': 13, 'first_frame': 1200}),
 }
 
 

@@ -2,6 +2,7 @@
 import hashlib
 import json
 import os
+import re
 import subprocess
 import sys
 
@@ -216,6 +217,10 @@ def test_cli_sharded_two_ranks_equal_single(tmp_path):
     for ext in ('.tbc', '.pcm', '.rgb'):
         assert (tmp_path / ('one' + ext)).read_bytes() == (tmp_path / ('two' + ext)).read_bytes(), ext
     assert json.load(open(tmp_path / 'one.json')) == json.load(open(tmp_path / 'two.json'))
+    # every epoch's windows hold O(epoch) samples, the last rank's too (not the rest of the capture)
+    wins = [(int(a), int(b)) for a, b in re.findall(r'capture window samples \[(\d+), (\d+)\)', r.stdout)]
+    spf = 1334668
+    assert len(wins) >= 2 * 3 and max(b - a for a, b in wins) <= 11 * spf + 1000001 + 2 * 16384 + 2048, wins
 
 
 @pytest.mark.gpu
@@ -275,6 +280,11 @@ def test_cli_epochs_resume_after_a_fault(tmp_path):
     for ext in ('.tbc', '.pcm', '.rgb'):
         assert (tmp_path / ('one' + ext)).read_bytes() == (tmp_path / ('ep' + ext)).read_bytes(), ext
     assert json.load(open(tmp_path / 'one.json')) == json.load(open(tmp_path / 'ep.json'))
+    # a rerun on the complete manifest is a no-op; another frame range is refused
+    r = run_cli('--comb', '--epoch-frames', '7', '--manifest', man, cap, tmp_path / 'ep')
+    assert r.returncode == 0 and 'already complete' in r.stdout, (r.stdout[-2000:], r.stderr[-2000:])
+    r = run_cli('--comb', '-s', '1', '--epoch-frames', '7', '--manifest', man, cap, tmp_path / 'ep')
+    assert r.returncode == 1 and 'belongs to another decode' in r.stdout
     with socket.socket() as sk:
         sk.bind(('127.0.0.1', 0))
         port = sk.getsockname()[1]
@@ -286,6 +296,10 @@ def test_cli_epochs_resume_after_a_fault(tmp_path):
     for ext in ('.tbc', '.pcm', '.rgb'):
         assert (tmp_path / ('one' + ext)).read_bytes() == (tmp_path / ('two' + ext)).read_bytes(), ext
     assert json.load(open(tmp_path / 'one.json')) == json.load(open(tmp_path / 'two.json'))
+    # every epoch's windows hold O(epoch) samples, the last rank's too (not the rest of the capture)
+    wins = [(int(a), int(b)) for a, b in re.findall(r'capture window samples \[(\d+), (\d+)\)', r.stdout)]
+    spf = 1334668
+    assert len(wins) >= 2 * 3 and max(b - a for a, b in wins) <= 11 * spf + 1000001 + 2 * 16384 + 2048, wins
 
 
 @pytest.mark.gpu

@@ -62,6 +62,51 @@ def test_demod_channels(decoded):
             assert np.abs(g - o).max() < 1e-3, ch
 
 
+MTF_LEVELS = [0.88, 0.5, 0.0]
+
+
+@pytest.mark.parametrize('system', ['NTSC', 'PAL'])
+def test_rf_table_mtf_levels(system, gpu_ctx_ntsc, gpu_ctx_pal):
+    """The demod's RF filter at MTF levels away from 1 (lddecode_core.py:290-293): the
+    ldg_k_rf_table path exp(m log|MTF|) cis(m arg MTF) against numpy's complex power
+    RFVideo * MTF**m of the oracle's filter set, and RFVideo alone at m = 0 (demodblock
+    skips the product there)."""
+    from oracle.demod import RFDemod
+    ctx, _ = gpu_ctx_ntsc if system == 'NTSC' else gpu_ctx_pal
+    F = RFDemod(system=system).Filters
+    for m in MTF_LEVELS + [1.0]:
+        got = ctx.rf_table(m)
+        ref = F['RFVideo'] * (F['MTF'] ** m) if m != 0 else F['RFVideo']
+        scale = np.abs(ref).max()
+        assert np.abs(got - ref).max() / scale < 1e-14, m
+    assert np.array_equal(ctx.rf_table(0.0), F['RFVideo'])
+
+
+@pytest.mark.parametrize('mtf', MTF_LEVELS)
+def test_demod_channels_at_mtf(mtf, cav_capture, gpu_ctx_ntsc):
+    """One field read demodulated at MTF 0.88, 0.5 and 0 (the m = 0 skip): channels within
+    1e-9 relative of the oracle's demod at the same level, peaks exact."""
+    _, data = cav_capture
+    ctx, rf = gpu_ctx_ntsc
+    buf = np.frombuffer(data, np.uint8)
+    ctx.set_capture(buf, buf.size, 0, 0)
+    infos = ctx.decode_reads([1052829], [mtf], slots=[7])     # slot 7: the module's fixtures use 0..3
+    from oracle.capture import FMT_U8, Capture
+    from oracle.demod import RFDemod
+    from oracle.field import FieldNTSC
+    orf = RFDemod(system='NTSC')
+    raw = orf.demod(Capture(data, FMT_U8), 1052829, 1000000, mtf)
+    f = FieldNTSC(orf, raw, 0, audio_offset=0)
+    for ci, ch in enumerate(['demod', 'demod_05', 'demod_sync', 'demod_burst']):
+        o = raw[0][ch]
+        g = ctx.debug(7, ci, np.float64, o.size)
+        assert g.size == o.size
+        assert np.abs(g - o).max() / max(np.abs(o).max(), 1.0) < 1e-9, (mtf, ch)
+    assert infos[0].npeaks == len(f.peaklist)
+    assert np.array_equal(ctx.debug(7, 41, np.int32, infos[0].npeaks), np.asarray(f.peaklist))
+    assert infos[0].nextfieldoffset == f.nextfieldoffset
+
+
 def test_field_records(decoded):
     ctx, infos, ref = decoded
     for slot, (raw, f) in enumerate(ref):
@@ -178,7 +223,10 @@ def test_pal_field_records_and_pilot_refine(decoded_pal):
 
 
 CASES = ['ntsc_cav_u8_0p2s', 'ntsc_clv_u8_0p2s', 'ntsc_cav_r30_0p15s', 'ntsc_cav_lds_0p15s', 'pal_clv_u8_0p2s',
-         'ntsc_cav_s16_0p15s', 'ntsc_cav_u8_mid_0p2s']
+         'ntsc_cav_s16_0p15s', 'ntsc_cav_u8_mid_0p2s',
+         # the MTF chain: a first frame re-read at MTF 0.88 (NTSC and PAL), the clamp to 0
+         'ntsc_cav_u8_mtf_0p3s', 'ntsc_cav_u8_mtf0_0p3s', 'pal_cav_u8_mtf_0p3s']
+MTF_CASES = CASES[-3:]
 _ORACLE = {}
 
 

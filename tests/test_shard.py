@@ -189,6 +189,22 @@ def test_shard_windows_cover_every_shards_reads():
             assert cut == hi == n
 
 
+def test_last_window_ends_with_the_decode_not_the_capture():
+    """An epoch of a long capture (the frame limit ends far before the capture) keeps the
+    last rank's window O(epoch) too; a read past it widens around the read."""
+    from ldgpu.shard import READ_SPAN, widen_window
+    n = 3600 * 40_000_000                                  # an hour of u8 RF
+    b, limit, _ = decode_bounds(n, n, SPF, 4, start_frame=5000, length=9)
+    w = shard_windows(b, SPF, n)
+    assert limit == 9
+    for lo, cut, hi in w:
+        assert hi - lo <= (9 // 4 + 2 + 2 + 2 + 1) * SPF + READ_SPAN + 1024 + 24
+    assert w[-1][1] == w[-1][2] < n
+    lo, hi = widen_window(w[-1][2] + 5 * SPF, SPF, n)
+    assert lo <= w[-1][2] + 4 * SPF - 1024 and hi >= w[-1][2] + 13 * SPF + READ_SPAN and hi - lo < 11 * SPF
+    assert widen_window(n - 100, SPF, n)[1] == n
+
+
 def _halo_worker(rank, world, port, fmt, q):
     import torch
     from ldgpu.shard import torch_p2p
@@ -381,7 +397,12 @@ def _clv_1s():
 
 @pytest.mark.gpu
 @pytest.mark.parametrize('world', [2, 3, 4])
-@pytest.mark.parametrize('case', ['ntsc_clv_u8_0p2s', 'clv_1s'])
+@pytest.mark.parametrize('case', ['ntsc_clv_u8_0p2s', 'clv_1s',
+                                  # the MTF chain across rank boundaries: every rank after the
+                                  # first starts from a fresh framer (MTF 1), so its warm-up frame
+                                  # re-reads at MTF 0.88 / 0.0002, and the clamp to 0 falls on a
+                                  # later rank (lddecode_core.py:1300-1309)
+                                  'ntsc_cav_u8_mtf_0p3s', 'ntsc_cav_u8_mtf0_0p3s'])
 def test_sharded_decode_vs_oracle(case, world):
     """Config 5's decode (field-group sharded, capture windows, ranks one after another on
     one device) against the ORACLE's single decode of the same capture -- not against
