@@ -217,10 +217,6 @@ def test_cli_sharded_two_ranks_equal_single(tmp_path):
     for ext in ('.tbc', '.pcm', '.rgb'):
         assert (tmp_path / ('one' + ext)).read_bytes() == (tmp_path / ('two' + ext)).read_bytes(), ext
     assert json.load(open(tmp_path / 'one.json')) == json.load(open(tmp_path / 'two.json'))
-    # every epoch's windows hold O(epoch) samples, the last rank's too (not the rest of the capture)
-    wins = [(int(a), int(b)) for a, b in re.findall(r'capture window samples \[(\d+), (\d+)\)', r.stdout)]
-    spf = 1334668
-    assert len(wins) >= 2 * 3 and max(b - a for a, b in wins) <= 11 * spf + 1000001 + 2 * 16384 + 2048, wins
 
 
 @pytest.mark.gpu
