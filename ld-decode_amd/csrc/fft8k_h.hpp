@@ -6,12 +6,14 @@
 // 16 points:
 //   * natural layout (transform input / inverse output): v[r] = x[t + 512 r];
 //   * spectral layout (transform output / inverse input): wave w owns the two
-//     512-point sub-arrays q0(w) = w and q1(w) = (16 - w) mod 16 | 8 for w = 0
-//     ({0,8}, {1,15}, {2,14}, ..., {7,9}) of the bins k = q + 16 j, and
-//       v[8 s + d] = X[q_s(w) + 16 k1 + 128 c + 1024 d],  lane = c + 8 k1.
-//     So bin k and its mirror 8192 - k live in the same wave (the real-FFT
-//     split / merge needs no workgroup exchange): for w > 0 the mirror of
-//     (s, lane, d) is (1 - s, 63 - lane, 7 - d).
+//     512-point sub-arrays q0(w) = w and q1(w) = 16 - w (8 for w = 0) of the
+//     bins k = q + 16 j, j = jl + 64 d with jl = (l >> 3) + 8 (l & 7):
+//       v[d]     = X[q0 + 16 (jl + 64 d)],
+//       v[8 + d] = X[q1 + 16 (jl + 64 d)]                 (w = 0),
+//       v[8 + d] = X[8192 - (q0 + 16 (jl + 64 (7 - d)))]  (w > 0: sub-array 1
+//                  lane-reversed, so v[15 - d] is the mirror bin of v[d]).
+//     bin_of() gives the bin of any position.  A real-FFT split / merge pairs
+//     bin k with 8192 - k: in the same thread for w > 0, in the same wave for w = 0.
 // Forward: radix-16 over r in registers, the stage twiddle W_8192^(q t), a
 // workgroup exchange through the 64 KiB buffer in two rounds (round s moves
 // every wave's sub-array s: 8 points per thread out, 8 in, so no thread holds
@@ -28,9 +30,18 @@ namespace h8k {
 constexpr int T = 512;                 // threads
 constexpr int EX = 4096;               // exchange buffer, double2 (64 KiB)
 
-__device__ __forceinline__ constexpr int q_of(int w, int s) { return s == 0 ? w : (w == 0 ? 8 : 16 - w); }
-// exchange slot (0..7) of sub-array q in its round (round = the sub-array index s)
-__device__ __forceinline__ constexpr int slot_of_q(int q) { return q < 8 ? q : (q == 8 ? 0 : 16 - q); }
+__host__ __device__ __forceinline__ constexpr int q_of(int w, int s) { return s == 0 ? w : (w == 0 ? 8 : 16 - w); }
+
+// the bin held at spectral-layout position (wave w, sub-array s, lane l, register d)
+__host__ __device__ __forceinline__ constexpr int bin_of(int w, int s, int l, int d) {
+  const int jl = (l >> 3) + 8 * (l & 7);
+  return s == 0 ? w + 16 * (jl + 64 * d)
+                : (w == 0 ? 8 + 16 * (jl + 64 * d) : 8192 - (w + 16 * (jl + 64 * (7 - d))));
+}
+// index of a per-position table (a wave's load of one register: 64 consecutive entries)
+__host__ __device__ __forceinline__ constexpr int pos_of(int w, int s, int l, int d) {
+  return ((w * 2 + s) * 8 + d) * 64 + l;
+}
 
 // wave-private transpose position: element e (0..7) of lane L, conflict-free for
 // ds_read_b128 by lane (16-lane groups) and for the writes of both transposes
@@ -51,15 +62,16 @@ __device__ __forceinline__ void wsync() {
 }
 
 // T1 (lane bits 3-5 <-> element) or T2 (lane bits 0-2 <-> element) of 8 points
-// through the wave's 8 KiB scratch sc.  Involutions.
+// through the wave's 8 KiB scratch sc.  Involutions.  lw / lr: the logical lane
+// the physical lane writes as / reads as (63 - l on the lane-reversed side).
 template <int BITS>   // 3: T1, 0: T2
-__device__ __forceinline__ void wtranspose(double2* v, double2* sc, int l) {
-  const int keep = l & ~(7 << BITS), mine = (l >> BITS) & 7;
+__device__ __forceinline__ void wtranspose(double2* v, double2* sc, int lw, int lr) {
+  const int keep = lw & ~(7 << BITS), mine = (lw >> BITS) & 7;
 #pragma unroll
   for (int e = 0; e < 8; e++) sc[tpos(keep | (e << BITS), mine)] = v[e];
   wsync();
 #pragma unroll
-  for (int e = 0; e < 8; e++) v[e] = sc[tpos(l, e)];
+  for (int e = 0; e < 8; e++) v[e] = sc[tpos(lr, e)];
   wsync();
 }
 
@@ -119,28 +131,29 @@ __device__ __forceinline__ void dft16_t(double2* v) {
 }
 
 // the 512-point sub-transform of sub-array s after the exchange: lane l holds
-// Y[l + 64 r'] in v[r'] -> X[k1 + 8 (c + 8 d)] in v[d], lane c + 8 k1
+// Y[l + 64 r'] in v[r'] -> X[k1 + 8 (c + 8 d)] in v[d] at lane c + 8 k1 (at
+// lane 63 - (c + 8 k1) when rev: the lane-reversed sub-array)
 template <bool INV>
-__device__ __forceinline__ void sub512_fwd(double2* v, double2* sc, const double2* __restrict__ tw, int l) {
+__device__ __forceinline__ void sub512_fwd(double2* v, double2* sc, const double2* __restrict__ tw, int l, bool rev) {
   asm volatile("" : "+v"(l));          // per-call addresses (not hoisted across the kernel's transforms)
   dft8<INV>(v);
   twiddle_row_w<8, INV>(v, tw[32 * l]);
-  wtranspose<3>(v, sc, l);             // lane (a, k1), elements b
+  wtranspose<3>(v, sc, l, l);          // lane (a, k1), elements b
   dft8<INV>(v);
   twiddle_row_w<8, INV>(v, tw[256 * (l & 7)]);
-  wtranspose<0>(v, sc, l);             // lane (c, k1), elements a
+  wtranspose<0>(v, sc, l, rev ? 63 - l : l);   // lane (c, k1), elements a
   dft8<INV>(v);
 }
 
 // inverse direction of sub512_fwd (its transpose)
 template <bool INV>
-__device__ __forceinline__ void sub512_inv(double2* v, double2* sc, const double2* __restrict__ tw, int l) {
+__device__ __forceinline__ void sub512_inv(double2* v, double2* sc, const double2* __restrict__ tw, int l, bool rev) {
   asm volatile("" : "+v"(l));
   dft8<INV>(v);
-  wtranspose<0>(v, sc, l);             // lane (a, k1), elements c
+  wtranspose<0>(v, sc, rev ? 63 - l : l, l);   // lane (a, k1), elements c
   twiddle_row_w<8, INV>(v, tw[256 * (l & 7)]);
   dft8<INV>(v);
-  wtranspose<3>(v, sc, l);             // lane (a, b), elements k1
+  wtranspose<3>(v, sc, l, l);          // lane (a, b), elements k1
   twiddle_row_w<8, INV>(v, tw[32 * l]);
   dft8<INV>(v);
 }
@@ -176,10 +189,10 @@ __device__ __forceinline__ void fwd(double2* v, double2* ex, const double2* __re
   __syncthreads();
 #pragma unroll
   for (int r = 0; r < 8; r++) v[8 + r] = mine[l + 64 * r];
-  sub512_fwd<INV>(v, mine, tw, l);
+  sub512_fwd<INV>(v, mine, tw, l, false);
 #pragma unroll
   for (int r = 8; r < 16; r++) pin(v[r]);   // the second sub-transform starts after the first (registers)
-  sub512_fwd<INV>(v + 8, mine, tw, l);
+  sub512_fwd<INV>(v + 8, mine, tw, l, w > 0);
   pin16(v);
 }
 
@@ -193,10 +206,10 @@ __device__ __forceinline__ void inv(double2* v, double2* ex, const double2* __re
   const int w = __builtin_amdgcn_readfirstlane(t >> 6), l = t & 63;
   double2* mine = ex + 512 * w;
   __syncthreads();                       // ex free of the previous phase
-  sub512_inv<INV>(v, mine, tw, l);
+  sub512_inv<INV>(v, mine, tw, l, false);
 #pragma unroll
   for (int r = 8; r < 16; r++) pin(v[r]);
-  sub512_inv<INV>(v + 8, mine, tw, l);
+  sub512_inv<INV>(v + 8, mine, tw, l, w > 0);
 #pragma unroll
   for (int r = 0; r < 8; r++) mine[l + 64 * r] = v[r];
   __syncthreads();

@@ -356,14 +356,21 @@ def windowed_decoders(data, fmt, system, world, batch=8, length=None):
     n = samples_in_bytes(fmt, raw.size)
     spf = decs[0].rf.samples_per_frame
     w = shard_windows(decode_bounds(n, raw.size, spf, world, length=length)[0], spf, n)
-    sds = []
-    for r, d in enumerate(decs):
-        lo, cut, hi = w[r]
+    from ldgpu.shard import widen_window
+
+    def load(d, lo, hi):
         b0 = sample_byte(fmt, lo)
         b1 = raw.size if hi >= n else sample_byte(fmt, hi)
         d.set_capture(raw[b0:b1], fmt, first_sample=lo, total_bytes=raw.size)
+
+    sds = []
+    for r, d in enumerate(decs):
+        lo, cut, hi = w[r]
+        load(d, lo, hi)
+        # the last rank's extension past its window widens it (lddecode.py widen_window)
         sds.append(ShardedDecode(d, r, world, length=length,
-                                 whole_capture=lambda d=d: d.set_capture(raw, fmt)))
+                                 whole_capture=lambda d=d: d.set_capture(raw, fmt),
+                                 widen=lambda s, d=d: load(d, *widen_window(s, spf, n))))
     return sds
 
 
@@ -447,6 +454,7 @@ def test_sharded_skipped_fields_extend_the_last_rank(world):
     sds = windowed_decoders(data, FMT_U8, 'NTSC', world, length=5)
     got, summ = run_ranks(sds)
     assert sds[-1].extended > 0
+    assert sds[-1].widened > 0          # the extension read past the last rank's capped window
     assert_matches_oracle(got, frames, pcm, meta)
 
 

@@ -57,11 +57,11 @@ __global__ __launch_bounds__(512, 4) void k_regs512(const double2* __restrict__ 
   double2* dst = out + (size_t)(blockIdx.x & 63) * M;
   if (REPS & 1) {
     // spectral layout -> natural bin order
-    const int w = t >> 6, l = t & 63, c = l & 7, k1 = l >> 3;
+    const int w = t >> 6, l = t & 63;
 #pragma unroll
     for (int s = 0; s < 2; s++)
 #pragma unroll
-      for (int d = 0; d < 8; d++) dst[h8k::q_of(w, s) + 16 * k1 + 128 * c + 1024 * d] = v[8 * s + d];
+      for (int d = 0; d < 8; d++) dst[h8k::bin_of(w, s, l, d)] = v[8 * s + d];
   } else {
 #pragma unroll
     for (int r = 0; r < 16; r++) dst[t + 512 * r] = v[r];
