@@ -34,6 +34,9 @@ using namespace ldg;
 
 namespace {
 
+#ifndef LDG_D2_WAVES
+#define LDG_D2_WAVES 4                   // waves per SIMD: two 512-thread workgroups per CU
+#endif
 #ifndef D2_STOP
 #define D2_STOP 99                       // (register-pressure experiments: return after phase D2_STOP)
 #endif
@@ -97,6 +100,9 @@ __device__ __forceinline__ int fr(int x) {
 }
 
 __device__ __forceinline__ void sqd(double& x) { asm volatile("" : "+v"(x)); }
+// pin z, and emit every memory access before this point here (the compiler would
+// otherwise sink a loop's park stores to its end, keeping all their data live)
+__device__ __forceinline__ void pinm(double2& z) { asm volatile("" : "+v"(z.x), "+v"(z.y)::"memory"); }
 
 __device__ __forceinline__ double fold_tau2(double d) {
   constexpr double TAU = 6.283185307179586;
@@ -114,22 +120,22 @@ __device__ __forceinline__ int w0_partner(int s, int l, int d) {
 
 // Store the pair of samples 2m, 2m+1 of a channel (o indexed by block position) if
 // kept ([BLOCKCUT, BLOCKCUT + copylen)); wave-uniform fast path as demod.hip.
-__device__ __forceinline__ void st_pair2(double* a, double2 z) {
+__device__ __forceinline__ void st_pair2(double* o, int p, double2 z) {
   typedef double v2d __attribute__((ext_vector_type(2)));
   const v2d zv = {z.x, z.y};
-  __builtin_nontemporal_store(zv, reinterpret_cast<v2d*>(a));
+  __builtin_nontemporal_store(zv, &h8k::at(reinterpret_cast<v2d*>(o), (unsigned)p >> 1));
 }
 __device__ __forceinline__ void store_pair2(double* o, int m, double2 z, int copylen) {
   const int p = 2 * m;
   const int pw0 = 2 * (m & ~63);
   if (pw0 >= BLOCKCUT && pw0 + 127 < BLOCKCUT + copylen) {
-    st_pair2(o + p, z);
+    st_pair2(o, p, z);
   } else if (pw0 + 127 >= BLOCKCUT && pw0 < BLOCKCUT + copylen) {
     const bool in0 = p >= BLOCKCUT && p < BLOCKCUT + copylen;
     const bool in1 = p + 1 >= BLOCKCUT && p + 1 < BLOCKCUT + copylen;
-    if (in0 && in1) *reinterpret_cast<double2*>(o + p) = z;
-    else if (in0) o[p] = z.x;
-    else if (in1) o[p + 1] = z.y;
+    if (in0 && in1) h8k::at(reinterpret_cast<double2*>(o), (unsigned)p >> 1) = z;
+    else if (in0) h8k::at(o, p) = z.x;
+    else if (in1) h8k::at(o, p + 1) = z.y;
   }
 }
 
@@ -138,13 +144,13 @@ __device__ __forceinline__ void store_pair05(double* o, int m, double2 z, int co
   const int p0 = (2 * m - BLOCKCUT_END) & (BLOCKLEN - 1);
   const int pw0 = (2 * (m & ~63) - BLOCKCUT_END) & (BLOCKLEN - 1);
   if (pw0 >= BLOCKCUT && pw0 + 127 < BLOCKCUT + copylen) {
-    st_pair2(o + p0, z);
+    st_pair2(o, p0, z);
   } else {
     const bool in0 = p0 >= BLOCKCUT && p0 < BLOCKCUT + copylen;
     const bool in1 = p0 + 1 >= BLOCKCUT && p0 + 1 < BLOCKCUT + copylen;
-    if (in0 && in1) *reinterpret_cast<double2*>(o + p0) = z;
-    else if (in0) o[p0] = z.x;
-    else if (in1) o[p0 + 1] = z.y;
+    if (in0 && in1) h8k::at(reinterpret_cast<double2*>(o), (unsigned)p0 >> 1) = z;
+    else if (in0) h8k::at(o, p0) = z.x;
+    else if (in1) h8k::at(o, p0 + 1) = z.y;
   }
 }
 
@@ -167,7 +173,7 @@ __device__ __forceinline__ void store_pair05(double* o, int m, double2 z, int co
   smap, reads, cap, cap_first, cap_nsamp, fmt, tw, twks, rf2, g2, g2m, iir, a_lfilt, a_rfilt, C, video,         \
       vread_stride, vchan_stride, status, parks, pbm, stiles, aslice, sst, sbits, bst, span
 
-template <bool CUT>
+template <bool CUT, bool PAL>
 __device__ __forceinline__ void demod2_body(LDG_DEMOD2_PARAMS) {
   __shared__ double2 ex[h8k::EX];                 // 64 KiB: exchanges, wave scratch, staging
   __shared__ uint16_t s_bits[BLOCKLEN / 16];       // sync detector bits (unrolled positions)
@@ -254,25 +260,28 @@ __device__ __forceinline__ void demod2_body(LDG_DEMOD2_PARAMS) {
   // E[k] = Y[k] + Y[k+M] (inverse-transformed in registers), O[k] = (Y[k] - Y[k+M])
   // conj(W^k) (parked).  Y[k+M] = conj(X[M-k]) F[k+M].
   double2* mine = ex + 512 * w;
-  double2* park = parks + (int64_t)s_park * P2_N;     // (s_park: set before the transform's barriers)
+  const int pslot = __builtin_amdgcn_readfirstlane(s_park);   // (set before the transform's barriers)
+  double2* park = parks + (int64_t)pslot * P2_N;
   const int a0 = C.audio_lo0;
   {
   const int l = fr(tid & 63), t = fr(tid);
   double2* as = aslice + ((int64_t)slot * MAX_BLOCKS_PER_READ + b) * 2048;   // left [0,1024), right [1024,2048)
   // one bin: X at bin k (Xk) and at M - k (Xm) -> E (returned), O (parked at register i), audio slices
-  auto analytic = [&](double2 Xk, double2 Xm, double2 wk, int pos, int k, int i) -> double2 {
-    const double2 y = cmul(Xk, F[pos]), yh = cmul(conj2(Xm), F[M5 + pos]);
-    park[P2_O + i * T5 + t] = cmulc(csub(y, yh), wk);
-    if (k >= a0 && k <= a0 + 512) {
+  // (aud: the register can hold an audio-slice bin -- bins < 2048 -- so the branch is
+  // compiled only there)
+  auto analytic = [&](double2 Xk, double2 Xm, double2 wk, int pos, int k, int i, bool aud) -> double2 {
+    const double2 y = cmul(Xk, h8k::at(F, pos)), yh = cmul(conj2(Xm), h8k::at(F, M5 + pos));
+    h8k::at(park, P2_O + i * T5 + t) = cmulc(csub(y, yh), wk);
+    if (aud && __builtin_expect(k >= a0 && k <= a0 + 512, 0)) {
       // audio_fdslice (lddecode_core.py:321-328): lo slot k - a0, hi (mirrored, conj) a0 + 1024 - k
       if (k < a0 + 512) {
-        as[k - a0] = cmul(Xk, a_lfilt[k - a0]);
-        as[1024 + k - a0] = cmul(Xk, a_rfilt[k - a0]);
+        h8k::at(as, k - a0) = cmul(Xk, h8k::at(a_lfilt, k - a0));
+        h8k::at(as, 1024 + k - a0) = cmul(Xk, h8k::at(a_rfilt, k - a0));
       }
       if (k > a0) {
         const int j = a0 + 1024 - k;
-        as[j] = cmul(conj2(Xk), a_lfilt[j]);
-        as[1024 + j] = cmul(conj2(Xk), a_rfilt[j]);
+        h8k::at(as, j) = cmul(conj2(Xk), h8k::at(a_lfilt, j));
+        h8k::at(as, 1024 + j) = cmul(conj2(Xk), h8k::at(a_rfilt, j));
       }
     }
     return cadd(y, yh);
@@ -285,38 +294,35 @@ __device__ __forceinline__ void demod2_body(LDG_DEMOD2_PARAMS) {
       const int l = fr(tid & 63);
       const int p0 = h8k::pos_of(w, 0, l, d), p1 = h8k::pos_of(w, 1, l, 7 - d);
       const double2 A = v[d], B = v[15 - d];
-      const double2 wk = twks[p0];
+      const double2 wk = h8k::at(twks, p0);
       const double2 Xk = rsplit2(A, B, wk), Xm = rsplit2(B, A, tw_mirror2(wk));
-      v[d] = analytic(Xk, Xm, wk, p0, h8k::bin_of(w, 0, l, d), d);
-      v[15 - d] = analytic(Xm, Xk, tw_mirror2(wk), p1, h8k::bin_of(w, 1, l, 7 - d), 15 - d);
+      v[d] = analytic(Xk, Xm, wk, p0, h8k::bin_of(w, 0, l, d), d, d < 2);
+      v[15 - d] = analytic(Xm, Xk, tw_mirror2(wk), p1, h8k::bin_of(w, 1, l, 7 - d), 15 - d, d >= 6);
       h8k::pin(v[d]);
-      h8k::pin(v[15 - d]);
+      pinm(v[15 - d]);
     }
   } else {
 #pragma unroll
     for (int s = 0; s < 2; s++) {
-      double2 P[8];
 #pragma unroll
       for (int d = 0; d < 8; d++) mine[d * 64 + l] = v[8 * s + d];
       h8k::wsync();
 #pragma unroll
-      for (int d = 0; d < 8; d++) P[d] = mine[w0_partner(s, l, d)];
-      h8k::wsync();
-#pragma unroll
       for (int d = 0; d < 8; d++) {
         const int l = fr(tid & 63);
+        const double2 P = mine[w0_partner(s, l, d)];   // (read before this register is overwritten: wave order)
         const int p = h8k::pos_of(0, s, l, d);
-        const double2 wk = twks[p];
-        const double2 Xk = rsplit2(v[8 * s + d], P[d], wk), Xm = rsplit2(P[d], v[8 * s + d], tw_mirror2(wk));
-        v[8 * s + d] = analytic(Xk, Xm, wk, p, h8k::bin_of(0, s, l, d), 8 * s + d);
-        h8k::pin(v[8 * s + d]);
+        const double2 wk = h8k::at(twks, p);
+        const double2 Xk = rsplit2(v[8 * s + d], P, wk), Xm = rsplit2(P, v[8 * s + d], tw_mirror2(wk));
+        v[8 * s + d] = analytic(Xk, Xm, wk, p, h8k::bin_of(0, s, l, d), 8 * s + d, d < 2);
+        pinm(v[8 * s + d]);
       }
     }
   }
 
   }
 
-  if (D2_STOP <= 2) { for (int i = 0; i < 16; i++) park[i * T5 + tid] = v[i]; return; }
+  if (D2_STOP <= 2) { for (int i = 0; i < 16; i++) h8k::at(park, i * T5 + tid) = v[i]; return; }
   // ---- 3. analytic IFFT halves -> instantaneous phase -> FM demod (Hz) ------------
   double th[16];
   h8k::inv<true>(v, ex, tw, t);                   // even samples y[2m]
@@ -328,13 +334,13 @@ __device__ __forceinline__ void demod2_body(LDG_DEMOD2_PARAMS) {
       h8k::pin(z);                                // one atan2 at a time (registers)
       double a = fast_atan2(z.y, z.x, s_atan);
       sqd(a);
-      reinterpret_cast<double*>(park + P2_TH)[r * T5 + t] = a;
+      h8k::at(reinterpret_cast<double*>(park + P2_TH), r * T5 + t) = a;
     }
   }
   {
     const int t = fr(tid);
 #pragma unroll
-    for (int i = 0; i < 16; i++) v[i] = park[P2_O + i * T5 + t];    // this thread's own parked entries
+    for (int i = 0; i < 16; i++) v[i] = h8k::at(park, P2_O + i * T5 + t);    // this thread's own parked entries
   }
   h8k::inv<true>(v, ex, tw, t);                   // odd samples y[2m + 1]
 #pragma unroll
@@ -355,14 +361,14 @@ __device__ __forceinline__ void demod2_body(LDG_DEMOD2_PARAMS) {
 #pragma unroll
     for (int r = 0; r < 16; r++) {
       const int m = t + T5 * r;
-      const double the = reinterpret_cast<const double*>(park + P2_TH)[r * T5 + t];
+      const double the = h8k::at(reinterpret_cast<const double*>(park + P2_TH), r * T5 + t);
       const double prev = m ? ph[m - 1] : 0.0;
       v[r] = make_double2(m ? fold_tau2(the - prev) * hzk : 0.0, fold_tau2(th[r] - the) * hzk);
     }
   }
   h8k::fwd<false>(v, ex, tw, t);
 
-  if (D2_STOP <= 3) { for (int i = 0; i < 16; i++) park[i * T5 + tid] = v[i]; return; }
+  if (D2_STOP <= 3) { for (int i = 0; i < 16; i++) h8k::at(park, i * T5 + tid) = v[i]; return; }
   // ---- 4. demod spectrum D (split) -> C2R spectra of demod_05 and video (merge) ------
   // P[k] = merge(D[k] G[k], D[M-k] G[M-k]); the video's is parked (unless past the cut)
   {
@@ -373,49 +379,46 @@ __device__ __forceinline__ void demod2_body(LDG_DEMOD2_PARAMS) {
       const int l = fr(tid & 63), t = fr(tid);
       const int p0 = h8k::pos_of(w, 0, l, d), p1 = h8k::pos_of(w, 1, l, 7 - d);
       const double2 A = v[d], B = v[15 - d];
-      const double2 wk = twks[p0], wm = tw_mirror2(wk);
+      const double2 wk = h8k::at(twks, p0), wm = tw_mirror2(wk);
       const double2 Dk = rsplit2(A, B, wk), Dm = rsplit2(B, A, wm);
-      const double4 Gk = g2[p0], Gm = g2[p1];
+      const double4 Gk = h8k::at(g2, p0), Gm = h8k::at(g2, p1);
       const double2 fk = cmul(Dk, make_double2(Gk.x, Gk.y)), fm = cmul(Dm, make_double2(Gm.x, Gm.y));
       v[d] = cmerge2(fk, fm, wk);
       v[15 - d] = cmerge2(fm, fk, wm);
       if (!vcut) {
         const double2 gk = cmul(Dk, make_double2(Gk.z, Gk.w)), gm = cmul(Dm, make_double2(Gm.z, Gm.w));
-        park[P2_V + d * T5 + t] = cmerge2(gk, gm, wk);
-        park[P2_V + (15 - d) * T5 + t] = cmerge2(gm, gk, wm);
+        h8k::at(park, P2_V + d * T5 + t) = cmerge2(gk, gm, wk);
+        h8k::at(park, P2_V + (15 - d) * T5 + t) = cmerge2(gm, gk, wm);
       }
       h8k::pin(v[d]);
-      h8k::pin(v[15 - d]);
+      pinm(v[15 - d]);
     }
   } else {
 #pragma unroll
     for (int s = 0; s < 2; s++) {
-      double2 P[8];
 #pragma unroll
       for (int d = 0; d < 8; d++) mine[d * 64 + l] = v[8 * s + d];
       h8k::wsync();
 #pragma unroll
-      for (int d = 0; d < 8; d++) P[d] = mine[w0_partner(s, l, d)];
-      h8k::wsync();
-#pragma unroll
       for (int d = 0; d < 8; d++) {
         const int l = fr(tid & 63), t = fr(tid);
+        const double2 P = mine[w0_partner(s, l, d)];
         const int p = h8k::pos_of(0, s, l, d);
-        const double2 wk = twks[p];
-        const double2 Dk = rsplit2(v[8 * s + d], P[d], wk), Dm = rsplit2(P[d], v[8 * s + d], tw_mirror2(wk));
-        const double4 Gk = g2[p], Gm = g2m[p];
+        const double2 wk = h8k::at(twks, p);
+        const double2 Dk = rsplit2(v[8 * s + d], P, wk), Dm = rsplit2(P, v[8 * s + d], tw_mirror2(wk));
+        const double4 Gk = h8k::at(g2, p), Gm = h8k::at(g2m, p);
         v[8 * s + d] = cmerge2(cmul(Dk, make_double2(Gk.x, Gk.y)), cmul(Dm, make_double2(Gm.x, Gm.y)), wk);
         if (!vcut)
-          park[P2_V + (8 * s + d) * T5 + t] =
+          h8k::at(park, P2_V + (8 * s + d) * T5 + t) =
               cmerge2(cmul(Dk, make_double2(Gk.z, Gk.w)), cmul(Dm, make_double2(Gm.z, Gm.w)), wk);
-        h8k::pin(v[8 * s + d]);
+        pinm(v[8 * s + d]);
       }
     }
   }
 
   }
 
-  if (D2_STOP <= 4) { for (int i = 0; i < 16; i++) park[i * T5 + tid] = v[i]; return; }
+  if (D2_STOP <= 4) { for (int i = 0; i < 16; i++) h8k::at(park, i * T5 + tid) = v[i]; return; }
   // ---- 5. demod_05 (C2R), its sync detector bits -> demod_sync (periodic IIR) ------
   const double inv = 1.0 / (double)M5;
   h8k::inv<true>(v, ex, tw, t);
@@ -507,10 +510,10 @@ __device__ __forceinline__ void demod2_body(LDG_DEMOD2_PARAMS) {
       }
     }
   }
-  if (D2_STOP <= 5) { for (int i = 0; i < 16; i++) park[i * T5 + tid] = v[i]; return; }
+  if (D2_STOP <= 5) { for (int i = 0; i < 16; i++) h8k::at(park, i * T5 + tid) = v[i]; return; }
   if (vcut) {
     __syncthreads();
-    if (tid == 0) park2_release(pbm, s_park);
+    if (tid == 0) park2_release(pbm, pslot);
     if (span && tid == 0) atomicMax(&span[1], (unsigned long long)__builtin_amdgcn_s_memrealtime());
     return;
   }
@@ -519,7 +522,7 @@ __device__ __forceinline__ void demod2_body(LDG_DEMOD2_PARAMS) {
   {
     const int t = fr(tid);
 #pragma unroll
-    for (int i = 0; i < 16; i++) v[i] = park[P2_V + i * T5 + t];
+    for (int i = 0; i < 16; i++) v[i] = h8k::at(park, P2_V + i * T5 + t);
   }
   h8k::inv<true>(v, ex, tw, t);
   const int t6 = fr(tid), l6 = fr(tid & 63);
@@ -560,8 +563,7 @@ __device__ __forceinline__ void demod2_body(LDG_DEMOD2_PARAMS) {
     const double2 eA = sos_chunk(x[0], hx[0].y, hx[0].x, zero, iir + 3, nullptr);
     const double2 eB = sos_chunk(x[1], hx[1].y, hx[1].x, zero, iir + 3, nullptr);
     double2 s_in[2];
-    iir2_scan2(eA, eB, pw, &s_aux, t6, iir2_pow(pw, l6), iir2_pow(pw, t6), iir2_pow(pw, scan_d15(l6)),
-               iir2_pow(pw, scan_d31(l6)), iir2_pow(pw, 512), &s_in[0], &s_in[1]);
+    iir2_scan2(eA, eB, pw, &s_aux, t6, &s_in[0], &s_in[1]);
 #pragma unroll
     for (int h = 0; h < 2; h++) {
       const int c = t6 + 512 * h;
@@ -571,14 +573,13 @@ __device__ __forceinline__ void demod2_body(LDG_DEMOD2_PARAMS) {
         bst[g] = make_double4(s_in[h].x, s_in[h].y, hx[h].y, hx[h].x);
       }
     }
-    if (C.n_chan > 4) {
+    if (PAL) {
       // PAL pilot from the same demod samples, stored at full rate from the chunk layout
       const double* pp = iir + IIR_MP;
       const double2 fA = sos_chunk(x[0], hx[0].y, hx[0].x, zero, iir + 8, nullptr);
       const double2 fB = sos_chunk(x[1], hx[1].y, hx[1].x, zero, iir + 8, nullptr);
       double2 p_in[2];
-      iir2_scan2(fA, fB, pp, &s_aux, t6, iir2_pow(pp, l6), iir2_pow(pp, t6), iir2_pow(pp, scan_d15(l6)),
-                 iir2_pow(pp, scan_d31(l6)), iir2_pow(pp, 512), &p_in[0], &p_in[1]);
+      iir2_scan2(fA, fB, pp, &s_aux, t6, &p_in[0], &p_in[1]);
       double* o = vout + (int64_t)CH_PILOT * vchan_stride;
 #pragma unroll
       for (int h = 0; h < 2; h++) {
@@ -588,22 +589,30 @@ __device__ __forceinline__ void demod2_body(LDG_DEMOD2_PARAMS) {
 #pragma unroll
         for (int i = 0; i < IIR_CHUNK; i += 2) {
           const int p = p0 + i;
-          if (p >= BLOCKCUT && p + 1 < BLOCKCUT + copylen) st_pair2(o + p, make_double2(y[i], y[i + 1]));
-          else if (p >= BLOCKCUT && p < BLOCKCUT + copylen) o[p] = y[i];
-          else if (p + 1 >= BLOCKCUT && p + 1 < BLOCKCUT + copylen) o[p + 1] = y[i + 1];
+          if (p >= BLOCKCUT && p + 1 < BLOCKCUT + copylen) st_pair2(o, p, make_double2(y[i], y[i + 1]));
+          else if (p >= BLOCKCUT && p < BLOCKCUT + copylen) h8k::at(o, p) = y[i];
+          else if (p + 1 >= BLOCKCUT && p + 1 < BLOCKCUT + copylen) h8k::at(o, p + 1) = y[i + 1];
         }
       }
     }
   }
   __syncthreads();
-  if (tid == 0) park2_release(pbm, s_park);
+  if (tid == 0) park2_release(pbm, pslot);
   if (span && tid == 0) atomicMax(&span[1], (unsigned long long)__builtin_amdgcn_s_memrealtime());
 }
 
-extern "C" __global__ __launch_bounds__(512, 4) void ldg_k_demod2(LDG_DEMOD2_PARAMS) { demod2_body<true>(LDG_DEMOD2_ARGS); }
-// the roofline leg's variant (ldg_demod_isolated): every block in full (no video cut)
-extern "C" __global__ __launch_bounds__(512, 4) void ldg_k_demod2_iso(LDG_DEMOD2_PARAMS) {
-  demod2_body<false>(LDG_DEMOD2_ARGS);
+extern "C" __global__ __launch_bounds__(512, LDG_D2_WAVES) void ldg_k_demod2(LDG_DEMOD2_PARAMS) {
+  demod2_body<true, false>(LDG_DEMOD2_ARGS);
+}
+extern "C" __global__ __launch_bounds__(512, LDG_D2_WAVES) void ldg_k_demod2_pal(LDG_DEMOD2_PARAMS) {
+  demod2_body<true, true>(LDG_DEMOD2_ARGS);
+}
+// the roofline leg's variants (ldg_demod_isolated): every block in full (no video cut)
+extern "C" __global__ __launch_bounds__(512, LDG_D2_WAVES) void ldg_k_demod2_iso(LDG_DEMOD2_PARAMS) {
+  demod2_body<false, false>(LDG_DEMOD2_ARGS);
+}
+extern "C" __global__ __launch_bounds__(512, LDG_D2_WAVES) void ldg_k_demod2_iso_pal(LDG_DEMOD2_PARAMS) {
+  demod2_body<false, true>(LDG_DEMOD2_ARGS);
 }
 
 // RF filter table for one mtf level in the register layout: entry pos < M holds

@@ -45,6 +45,17 @@ __host__ __device__ __forceinline__ constexpr int pos_of(int w, int s, int l, in
 
 // wave-private transpose position: element e (0..7) of lane L, conflict-free for
 // ds_read_b128 by lane (16-lane groups) and for the writes of both transposes
+// base[idx] through a 32-bit unsigned byte offset: with a uniform base the access is
+// global_load / store v_off, s[base] (one address VGPR instead of a 64-bit pair)
+template <class T>
+__device__ __forceinline__ T& at(T* base, unsigned idx) {
+  return *reinterpret_cast<T*>(reinterpret_cast<char*>(base) + idx * (unsigned)sizeof(T));
+}
+template <class T>
+__device__ __forceinline__ const T& at(const T* base, unsigned idx) {
+  return *reinterpret_cast<const T*>(reinterpret_cast<const char*>(base) + idx * (unsigned)sizeof(T));
+}
+
 __device__ __forceinline__ int tpos(int L, int e) { return 8 * L + (e ^ ((L >> 1) & 7)); }
 
 // Materialise a value here: the compiler may otherwise sink its arithmetic past
@@ -78,7 +89,7 @@ __device__ __forceinline__ void wtranspose(double2* v, double2* sc, int lw, int 
 // the stage twiddles W_8192^(q t), q = 1..15, applied to y[q] (conjugate: INV)
 template <bool INV>
 __device__ __forceinline__ void tw16(double2* y, const double2* __restrict__ tw, int t) {
-  double2 g1 = tw[2 * t], g2 = tw[4 * t], g4 = tw[8 * t], g8 = tw[16 * t];
+  double2 g1 = at(tw, 2 * t), g2 = at(tw, 4 * t), g4 = at(tw, 8 * t), g8 = at(tw, 16 * t);
   if (INV) { g1 = conj2(g1); g2 = conj2(g2); g4 = conj2(g4); g8 = conj2(g8); }
   const double2 g3 = cmul(g2, g1);
   y[1] = cmul(y[1], g1);
@@ -137,10 +148,10 @@ template <bool INV>
 __device__ __forceinline__ void sub512_fwd(double2* v, double2* sc, const double2* __restrict__ tw, int l, bool rev) {
   asm volatile("" : "+v"(l));          // per-call addresses (not hoisted across the kernel's transforms)
   dft8<INV>(v);
-  twiddle_row_w<8, INV>(v, tw[32 * l]);
+  twiddle_row_w<8, INV>(v, at(tw, 32 * l));
   wtranspose<3>(v, sc, l, l);          // lane (a, k1), elements b
   dft8<INV>(v);
-  twiddle_row_w<8, INV>(v, tw[256 * (l & 7)]);
+  twiddle_row_w<8, INV>(v, at(tw, 256 * (l & 7)));
   wtranspose<0>(v, sc, l, rev ? 63 - l : l);   // lane (c, k1), elements a
   dft8<INV>(v);
 }
@@ -151,10 +162,10 @@ __device__ __forceinline__ void sub512_inv(double2* v, double2* sc, const double
   asm volatile("" : "+v"(l));
   dft8<INV>(v);
   wtranspose<0>(v, sc, rev ? 63 - l : l, l);   // lane (a, k1), elements c
-  twiddle_row_w<8, INV>(v, tw[256 * (l & 7)]);
+  twiddle_row_w<8, INV>(v, at(tw, 256 * (l & 7)));
   dft8<INV>(v);
   wtranspose<3>(v, sc, l, l);          // lane (a, b), elements k1
-  twiddle_row_w<8, INV>(v, tw[32 * l]);
+  twiddle_row_w<8, INV>(v, at(tw, 32 * l));
   dft8<INV>(v);
 }
 

@@ -84,10 +84,10 @@ __device__ __forceinline__ double2 mat2(double4 m, double2 v, double2 acc) {
 }
 
 // Second order (Fburst / Fpilot): the same for 2-vector states (y[n], y[n-1]).
-// ml, mt, m15, m31: C^(16 lane), C^(16 t), C^(16 scan_d15), C^(16 scan_d31); m512: C^(16*512).
+// pw: the C^(16 s) table; the per-lane powers C^(16 lane), C^(16 t), C^(16 scan_d15),
+// C^(16 scan_d31) and C^(16*512) are loaded where they are used (registers).
 __device__ __forceinline__ void iir2_scan2(double2 eA, double2 eB, const double* __restrict__ pw, IIRAux2* aux, int tid,
-                                           double4 ml, double4 mt, double4 m15, double4 m31, double4 m512, double2* sA,
-                                           double2* sB) {
+                                           double2* sA, double2* sB) {
   const int lane = tid & 63, w = tid >> 6;
   carry_step<0x111, 2>(eA.x, eA.y, pw, 1);
   carry_step<0x111, 2>(eB.x, eB.y, pw, 1);
@@ -97,10 +97,16 @@ __device__ __forceinline__ void iir2_scan2(double2 eA, double2 eB, const double*
   carry_step<0x114, 2>(eB.x, eB.y, pw, 4);
   carry_step<0x118, 2>(eA.x, eA.y, pw, 8);
   carry_step<0x118, 2>(eB.x, eB.y, pw, 8);
-  carry_step_lane2<0x142, 0xa>(eA.x, eA.y, m15);
-  carry_step_lane2<0x142, 0xa>(eB.x, eB.y, m15);
-  carry_step_lane2<0x143, 0xc>(eA.x, eA.y, m31);
-  carry_step_lane2<0x143, 0xc>(eB.x, eB.y, m31);
+  {
+    const double4 m15 = iir2_pow(pw, scan_d15(lane));
+    carry_step_lane2<0x142, 0xa>(eA.x, eA.y, m15);
+    carry_step_lane2<0x142, 0xa>(eB.x, eB.y, m15);
+  }
+  {
+    const double4 m31 = iir2_pow(pw, scan_d31(lane));
+    carry_step_lane2<0x143, 0xc>(eA.x, eA.y, m31);
+    carry_step_lane2<0x143, 0xc>(eB.x, eB.y, m31);
+  }
   double2 a = make_double2(dpp_f64<0x138>(eA.x), dpp_f64<0x138>(eA.y));
   double2 b = make_double2(dpp_f64<0x138>(eB.x), dpp_f64<0x138>(eB.y));
   if (lane == 63) {
@@ -112,10 +118,13 @@ __device__ __forceinline__ void iir2_scan2(double2 eA, double2 eB, const double*
   iir_wave_carries2<2>(aux, pw, tid);
   const double2 TA = make_double2(aux->k[0][8][0], aux->k[0][8][1]);
   const double2 TB = make_double2(aux->k[1][8][0], aux->k[1][8][1]);
+  const double4 m512 = iir2_pow(pw, 512);
   const double2 S0 = mat2(m512, TA, TB);
   const double2 S512 = mat2(m512, S0, TA);
+  const double4 ml = iir2_pow(pw, lane);
   a = mat2(ml, make_double2(aux->k[0][w][0], aux->k[0][w][1]), a);
   b = mat2(ml, make_double2(aux->k[1][w][0], aux->k[1][w][1]), b);
+  const double4 mt = iir2_pow(pw, tid);
   *sA = mat2(mt, S0, a);
   *sB = mat2(mt, S512, b);
 }

@@ -7,8 +7,9 @@ all per-sample and per-line work runs as HIP kernels on gfx950.
 
 import os as _os
 
-# A context drives 6 HIP streams (demod, 2 field-chain sub-streams, audio phase 2,
-# frame/comb output, synchronous audio output).  HIP maps streams onto
+# A context drives 10 HIP streams (two demod streams, read setup, audio, records,
+# frame output, comb, synchronous output and 2 field-chain sub-streams,
+# INTEGRATION.md "Buffers and threading").  HIP maps streams onto
 # GPU_MAX_HW_QUEUES hardware queues (default 4); fewer queues than streams
 # serialises unrelated streams behind each other, so ask for 12 (room for 4 field-chain sub-streams) -- before the
 # HIP runtime initialises (the first HIP call in the process).
