@@ -188,6 +188,9 @@ def cpu_baseline(get_capture, fmt, system, frames, procs):
             tot = sum(r[0] for r in res)
             out['multi_process'] = {'value': tot / wall / 1e6, 'unit': 'RF Msamples/s', 'processes': procs,
                                     'cores': procs, 'fields_per_s': 2 * sum(r[1] for r in res) / wall,
+                                    'process_cap': ('min(16, CPUs visible): the GPU box allots each GPU a 16-CPU share '
+                                                    '(os.cpu_count() there shows the whole host, %d CPUs); '
+                                                    '--cpu-procs N overrides' % len(os.sched_getaffinity(0))),
                                     'sample': '%d slices of the benchmark capture%s, %d frames each, one process '
                                               '(one core) each, %.1f s wall' % (procs, note, frames, wall)}
     return out
@@ -371,6 +374,33 @@ class ShardedWorkload:
                               'first frame(s) from the exact state after the exchange (shard.comb_fix), '
                               'not timed here'}
 
+    def same_share_single(self, steps=2):
+        """Rank 0's share of the capture decoded by this GPU alone (no exchange, the other
+        ranks idle), in the same session: the N = 1 rate of the per-rank work, beside the
+        N-rank line (config 5's scaling then has a baseline on its own workload).
+        Returns (RF Msamples/s, ms per step, frames per step)."""
+        dec, lo, cut = self.dec, self.windows[self.rank][0], self.windows[self.rank][1]
+        if self.buf is not None and self.on_device:
+            dec.set_capture(None, 0, device_ptr=self.buf.data_ptr(), nsamples=self.windows[self.rank][2] - lo,
+                            first_sample=lo, total_bytes=self.total)
+        elif self.buf is not None:
+            dec.set_capture(self.buf.numpy(), 0, nsamples=self.windows[self.rank][2] - lo, first_sample=lo,
+                            total_bytes=self.total)
+        else:
+            dec.use_resident_capture(0, self.total)
+        out = []
+        for k in range(steps + 1):
+            dec._reset_cache()
+            t0 = time.perf_counter()
+            n = dec.decode(sink=None, comb=not self.args.no_comb, start_sample=lo, stop_sample=cut,
+                           firstframe=lo == 0)
+            dt = time.perf_counter() - t0
+            if k:                                   # the first pass warms up
+                out.append((dec.last_meta['nextsample'] - lo if dec.last_meta else 0, dt, n))
+        ns = sum(o[0] for o in out)
+        dt = sum(o[1] for o in out)
+        return ns / dt / 1e6, dt / len(out) * 1e3, out[-1][2]
+
     def checks(self):
         return {'frames_per_step_all_ranks': self.stats.get('frames_total'),
                 'chain_refixes': self.stats.get('refixes', 0), 'window_misses': self.stats.get('window_misses', 0),
@@ -496,6 +526,14 @@ def main():
     reads_timed = dec.stats['reads'] - reads0
     used_timed = dec.stats['reads_used'] - used0
     checks = wl.checks()
+    same_share = None
+    if dist is not None and isinstance(wl, ShardedWorkload):
+        # the N = 1 rate of the same per-rank work, rank 0 alone on its GPU (others wait)
+        barrier()
+        if rank == 0:
+            progress(rank, 'same-share single-GPU leg')
+            same_share = wl.same_share_single()
+        barrier()
 
     if dist is not None:
         import torch
@@ -600,6 +638,15 @@ def main():
                                for k in ('plan_s', 'gpu_s', 'replay_s', 'flush_s', 'wait_s')},
                        inflight_at_wait=dec.stats.get('inflight_at_wait')),
     }
+    if world > 1:
+        line['per_rank_value'] = round(msps / world, 3)
+        if same_share is not None:
+            line['same_share_n1'] = {
+                'value': round(same_share[0], 3), 'unit': 'RF Msamples/s', 'ms_per_step': round(same_share[1], 3),
+                'frames_per_step': same_share[2],
+                'note': ("rank 0's share of this capture (1/%d) decoded by one GPU alone in this session, no "
+                         'exchange: the N = 1 rate of the per-rank work, so the N-rank value has a baseline on '
+                         'its own workload (N x this = perfect scaling)' % world)}
     print(json.dumps(line), flush=True)
     if dist is not None:
         dist.destroy_process_group()

@@ -207,8 +207,8 @@ class GPUDecoder:
         # predicts exactly, so a deeper speculation costs no reads.  PAL 3: 4 was
         # 3-7% slower (more reads in flight over its start-up wander)
         self.depth = int(os.environ.get('LDG_DEPTH', '4' if self.sysp.name == 'NTSC' else '3'))
-        if not 1 <= self.depth <= 4:
-            raise ValueError('LDG_DEPTH must be 1..4')
+        if not 1 <= self.depth <= 7:
+            raise ValueError('LDG_DEPTH must be 1..7')
         self.capacity = capacity or max((self.depth + 2) * batch, batch + 16)
         self.ctx = native.Context(system, device, max_reads=self.capacity, max_frames=self.capacity)
         self.ctx.set_filters(self.rf.params(), self.rf.tables)
