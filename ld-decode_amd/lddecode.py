@@ -97,8 +97,8 @@ def main(argv=None):
             torch.cuda.set_device(local)
         dist.init_process_group('cpu:gloo,cuda:nccl' if rccl else 'gloo')
         args.device = local % max(1, ndev)
-        if args.comb and (system != 'NTSC' or args.comb_3d):
-            print("ERROR: a sharded decode runs the 2D NTSC comb only")
+        if args.comb and args.comb_3d:
+            print("ERROR: a sharded decode runs the 2D comb (NTSC) or the PAL Y/C decoder only")
             return 1
     dec = GPUDecoder(system=system, device=args.device, batch=args.batch)
     if args.comb_args:
@@ -146,8 +146,8 @@ def main(argv=None):
 
     num_frames = req_frames if req_frames is not None else infile_size // bytes_per_frame - firstframe
     if world > 1 or args.epoch_frames or args.manifest:
-        if args.comb and (system != 'NTSC' or args.comb_3d):
-            print("ERROR: a sharded or epoch-wise decode runs the 2D NTSC comb only")
+        if args.comb and args.comb_3d:
+            print("ERROR: a sharded or epoch-wise decode runs the 2D comb (NTSC) or the PAL Y/C decoder only")
             return 1
         if dec.ctx.comb_width != 744:
             print("ERROR: a sharded or epoch-wise decode does not hand comb-ntsc -W's Y-NR history across pieces")
@@ -234,6 +234,10 @@ def widen_window(dec, raw, fmt, rccl, sample, keep):
         dec.set_capture(buf.numpy(), fmt, first_sample=lo, total_bytes=nbytes)
     keep[:] = [buf]
     print('capture window widened to samples [%d, %d)' % (lo, hi))
+
+
+def system_of(dec):
+    return dec.sysp.name
 
 
 def write_manifest(path, man):
@@ -327,7 +331,7 @@ def sharded(args, dec, outname, firstframe, num_frames, nextsample, req_frames, 
             fh.writelines(lines)
     barrier()
     frame_bytes = dec.sysp.outlinelen * dec.sysp.frame_lines * 2
-    rgb_bytes = dec.ctx.comb_width * dec.ctx.comb_lines * 3 * 2
+    rgb_bytes = (1057 * 576 if system_of(dec) == 'PAL' else dec.ctx.comb_width * dec.ctx.comb_lines) * 3 * 2
     epoch_frames = args.epoch_frames or num_frames
     stats = {}
     while not man['complete'] and man['frames'] < num_frames:
@@ -362,8 +366,9 @@ def sharded(args, dec, outname, firstframe, num_frames, nextsample, req_frames, 
             # combed in HBM during the decode; the burst-level EMA (comb-ntsc.cxx:560-566,
             # global over every frame) was handed across the ranks and the first frames
             # re-combed with it (ldgpu/shard.py comb_fix)
-            print('rank %d: comb re-combed %d frame(s) with the exact burst-level state' %
-                  (rank, stats.get('comb_recombed_frames', 0)))
+            if system_of(dec) == 'NTSC':
+                print('rank %d: comb re-combed %d frame(s) with the exact burst-level state' %
+                      (rank, stats.get('comb_recombed_frames', 0)))
             with open(outname + '.rgb', 'r+b') as fh:
                 fh.seek(first * rgb_bytes)
                 for r in res:

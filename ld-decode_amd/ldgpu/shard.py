@@ -555,7 +555,10 @@ def _decode_sharded(dec, rank, world, allgather, sink, start_frame, length, star
     t2 = time.perf_counter()
     res = sd.finish(summ)
     a0 = None
-    if sd.rgb is not None:
+    if sd.rgb is not None and dec.sysp.name == 'NTSC':
+        # the NTSC comb's burst-level EMA spans every frame (comb_fix); the PAL Y/C
+        # decoder's is a constant-input chain at its fixed point from the first line
+        # (csrc/combpal.hip pal_angle), so a PAL rank's frames comb exactly on their own
         a0 = comb_fix(sd, allgather, len(res), stats)
     if epoch_end is not None:
         # the exact state after the decode's last output frame (the next epoch's init)

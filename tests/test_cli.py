@@ -220,6 +220,33 @@ def test_cli_sharded_two_ranks_equal_single(tmp_path):
 
 
 @pytest.mark.gpu
+def test_cli_sharded_pal_equal_single(tmp_path):
+    """PAL sharded too: 3 ranks on a PAL CLV capture write the same .tbc /
+    .pcm / .json and, with --comb, the same PAL Y/C .rgb as one process (the Y/C decoder's
+    burst-level chain is at its fixed point from the first line, so ranks comb on their own);
+    and 2 ranks with --epoch-frames too."""
+    import socket
+    from ldgpu.synth import make_capture
+    data = make_capture(int(40e6 * 0.8), 'u8', system='PAL', clv=True, first_frame=4200, seed=17)
+    cap = tmp_path / 'cap.u8'
+    cap.write_bytes(bytes(data))
+    r = run_cli('-p', '--comb', cap, tmp_path / 'one')
+    assert r.returncode == 0, r.stderr[-2000:]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY='0')
+    for name, extra, n in (('three', [], 3), ('ep', ['--epoch-frames', '5'], 2)):
+        with socket.socket() as sk:
+            sk.bind(('127.0.0.1', 0))
+            port = sk.getsockname()[1]
+        r = subprocess.run([sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', '--nproc-per-node', str(n),
+                            '--master-addr', '127.0.0.1', '--master-port', str(port), CLI, '-p', '--comb'] + extra +
+                           [str(cap), str(tmp_path / name)], capture_output=True, text=True, timeout=600, env=env)
+        assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-3000:])
+        for ext in ('.tbc', '.pcm', '.rgb'):
+            assert (tmp_path / ('one' + ext)).read_bytes() == (tmp_path / (name + ext)).read_bytes(), (name, ext)
+        assert json.load(open(tmp_path / 'one.json')) == json.load(open(tmp_path / (name + '.json'))), name
+
+
+@pytest.mark.gpu
 def test_cli_sharded_fused_comb_recombs_only_the_first_frames(tmp_path):
     """Three ranks with --comb on a 2 s capture: each rank combs its frames in HBM as they
     are decoded (ldg_output_async) from a "not initialised" burst-level EMA, then re-combs

@@ -409,7 +409,9 @@ def _clv_1s():
                                   # first starts from a fresh framer (MTF 1), so its warm-up frame
                                   # re-reads at MTF 0.88 / 0.0002, and the clamp to 0 falls on a
                                   # later rank (lddecode_core.py:1300-1309)
-                                  'ntsc_cav_u8_mtf_0p3s', 'ntsc_cav_u8_mtf0_0p3s'])
+                                  'ntsc_cav_u8_mtf_0p3s', 'ntsc_cav_u8_mtf0_0p3s',
+                                  # PAL: the same field-group windows and chains
+                                  'pal_clv_u8_0p2s', 'pal_cav_u8_mtf_0p3s'])
 def test_sharded_decode_vs_oracle(case, world):
     """Config 5's decode (field-group sharded, capture windows, ranks one after another on
     one device) against the ORACLE's single decode of the same capture -- not against
