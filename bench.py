@@ -47,6 +47,15 @@ HBM_PEAK_GBS = 8000.0
 FP64_PEAK_TFLOPS = 78.6                           # MI355X FP64 vector (spec)
 READ_BLOCKS = 66                                  # overlap-save blocks per 1e6-sample field read
 ISO_ITERS = 20                                    # launches of the isolated roofline leg
+# the leg's kernels: ldg_k_demod_iso (full blocks) and ldg_k_demod_iso_cut (the shipped body);
+# the 512-thread demod (LDG_DEMOD2=1, experimental) has the first only
+ISO_VARIANTS = (0,) if os.environ.get('LDG_DEMOD2', '0') != '0' else (0, 1)
+
+
+def iso_leg(dec):
+    """(reads, full-body ms, shipped-body ms or None) of the isolated roofline leg"""
+    reads, ms = dec.demod_isolated(ISO_ITERS, ISO_VARIANTS)
+    return (reads, ms, None) if len(ISO_VARIANTS) == 1 else (reads, ms[0], ms[1])
 # the FFT flops the demod executes per block (5 N log2 N): six 8192-point complex transforms
 # (raw R2C, analytic even / odd, demod R2C, C2R 0.5 MHz, C2R video) + two 1024-point audio IFFTs;
 # sync / burst / pilot are time-domain recurrences (iir.hpp) and are not counted
@@ -199,7 +208,7 @@ def cpu_baseline(get_capture, fmt, system, frames, procs):
 LDS_PEAK_TBS = 150.0          # ds_read_b64/b128 with every CU streaming (MI355X_MICROARCH.md, LDS)
 
 
-def bound_analysis(sq, traffic, iso_ms):
+def bound_analysis(sq, traffic, iso_ms, name='demod_iso_sq'):
     """Which resource the demod sits against, from the committed PMC passes over the same
     isolated leg (profiles/pmc_traffic.json, tools/pmc_summary.py) and this run's launch time:
     HBM (PMC bytes / time), LDS (ds bytes / time against ~150 TB/s, and LDS-array busy
@@ -220,7 +229,7 @@ def bound_analysis(sq, traffic, iso_ms):
         out['lds_bytes_per_launch'] = d['lds_bytes']
         out['lds_tbs'] = d['lds_bytes'] / (iso_ms * 1e-3) / 1e12
         out['lds_frac'] = out['lds_tbs'] / LDS_PEAK_TBS
-    out['source'] = 'profiles/pmc_traffic.json demod_iso_sq (rocprofv3 --pmc passes over this bench\'s isolated leg)'
+    out['source'] = 'profiles/pmc_traffic.json %s (rocprofv3 --pmc passes over this bench\'s isolated leg)' % name
     return out
 
 
@@ -519,10 +528,10 @@ def main():
         for r in range(world):
             barrier()
             if r == rank:
-                iso_reads, iso_ms = dec.demod_isolated(ISO_ITERS)
+                iso_reads, iso_ms, cut_ms = iso_leg(dec)
         barrier()
     else:
-        iso_reads, iso_ms = dec.demod_isolated(ISO_ITERS)
+        iso_reads, iso_ms, cut_ms = iso_leg(dec)
     reads_timed = dec.stats['reads'] - reads0
     used_timed = dec.stats['reads_used'] - used0
     checks = wl.checks()
@@ -568,7 +577,7 @@ def main():
     samples_per_read = consumed / max(used_timed, 1)
     units_iso = iso_reads * samples_per_read
     achieved = bps * units_iso / (iso_ms * 1e-3) / 1e9
-    traffic, lds = None, None
+    traffic, lds, traffic_cut, lds_cut = None, None, None, None
     # the committed --pmc passes of this system's bench command (PAL stores the pilot channel too)
     pmc = os.path.join(ROOT, 'profiles', 'pmc_traffic_pal.json' if pal else 'pmc_traffic.json')
     if os.path.exists(pmc):
@@ -576,8 +585,10 @@ def main():
             pj = json.load(open(pmc))
             traffic = pj['kernels'].get('demod_iso')
             lds = bound_analysis(pj.get('demod_iso_sq'), traffic, iso_ms)
+            traffic_cut = pj['kernels'].get('demod_iso_cut')
+            lds_cut = bound_analysis(pj.get('demod_iso_cut_sq'), traffic_cut, cut_ms, 'demod_iso_cut_sq')
         except Exception:
-            traffic = None
+            traffic = traffic_cut = None
     # the pipeline's own demod launches (co-running with the field kernels, two demod streams
     # overlapping consecutive launches): in-kernel execution spans and HIP-event intervals
     dom_launches, dom_ms = stats.get('demod', (1, float('nan')))
@@ -604,6 +615,13 @@ def main():
         'traffic_unit': 'bytes per launch, 2*FETCH_SIZE + WRITE_SIZE (profiles/%s, demod_iso)' % os.path.basename(pmc),
         'traffic_x_algorithmic': (traffic / (bps * units_iso)) if traffic else None,
         'issue': lds, 'fp64': fp64,
+        'production': {
+            'kernel': 'ldg_k_demod_iso_cut: the shipped demod body (ldg_k_demod, video cut) under its own symbol, '
+                      'same reads, launches and units as the leg above',
+            'avg_launch_ms': round(cut_ms, 4) if cut_ms else None,
+            'achieved': round(bps * units_iso / (cut_ms * 1e-3) / 1e9, 4) if cut_ms else None,
+            'frac': bps * units_iso / (cut_ms * 1e-3) / 1e9 / HBM_PEAK_GBS if cut_ms else None,
+            'traffic': traffic_cut, 'issue': lds_cut},
         'pipeline': {'launches': dom_launches, 'span_ms': round(span_ms, 4), 'hip_event_ms': round(event_ms, 4),
                      'busy_ms_per_launch': round(busy_ms, 4), 'units_per_launch': round(units_pipe),
                      'achieved_busy': round(bps * units_pipe / (busy_ms * 1e-3) / 1e9, 4),

@@ -348,6 +348,11 @@ int ldg_profile_spans_union(ldg_ctx* ctx, double* union_ms, int64_t* count);
  * *ms_per_launch = the mean HIP-event duration of a launch.  The slots' demod
  * outputs are recomputed in place (a host read cache should be dropped). */
 int ldg_demod_isolated(ldg_ctx* ctx, int n, const int32_t* slots, int iters, double* ms_per_launch);
+/* The same leg by variant: 0 = ldg_k_demod_iso (as above, every block in full),
+ * 1 = ldg_k_demod_iso_cut, the shipped body of ldg_k_demod (blocks past a read's
+ * video cut stop after the sync channel) under its own symbol.  LDG_EINVAL for
+ * other variants, and for 1 when the 512-thread demod (LDG_DEMOD2) is selected. */
+int ldg_demod_isolated_ex(ldg_ctx* ctx, int n, const int32_t* slots, int iters, int variant, double* ms_per_launch);
 
 /* ---- benchmark / test tooling (not a reference interface) ----------------------
  * Synthesise an NTSC LaserDisc RF capture directly into this context's HBM

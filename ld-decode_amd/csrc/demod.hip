@@ -723,6 +723,8 @@ extern "C" __global__ __launch_bounds__(1024) void ldg_k_demod(LDG_DEMOD_PARAMS)
 // events, undisturbed by the field kernels that co-run with ldg_k_demod.  It
 // demodulates every block in full (no video cut): the leg times whole reads.
 extern "C" __global__ __launch_bounds__(1024) void ldg_k_demod_iso(LDG_DEMOD_PARAMS) { demod_body<false>(LDG_DEMOD_ARGS); }
+// The shipped body (video cut) for the same leg: ldg_demod_isolated_ex variant 1.
+extern "C" __global__ __launch_bounds__(1024) void ldg_k_demod_iso_cut(LDG_DEMOD_PARAMS) { demod_body<true>(LDG_DEMOD_ARGS); }
 
 // ---------------------------------------------------------------------------
 // Audio phase 1 (lddecode_core.py:321-328): per overlap-save block, the two

@@ -548,21 +548,25 @@ class GPUDecoder:
         if len(h) < 64:
             h.append(best)
 
-    def demod_isolated(self, iters=10):
+    def demod_isolated(self, iters=10, variants=(0,)):
         """(reads, ms per launch) of the demod alone over `batch` decoded reads,
         `iters` launches back to back (the benchmark's roofline leg).  The reads are the
         most recent cached reads whose field decoded (FS_VALID): every block of such a
         read lies inside the resident capture, so each launch demodulates whole reads
         (a sharded rank's speculative reads past its window are FS_EOF and their
         workgroups would return at once; the library refuses them).  The reads' demod
-        outputs are recomputed in place, so the read cache is dropped."""
+        outputs are recomputed in place, so the read cache is dropped.  `variants`
+        (native.Context.demod_isolated) run in turn over the same reads; with more than
+        one the ms figure is a list in that order."""
         slots = [sl for sl, inf in reversed(list(self.cache.values())) if inf.status == native.FS_VALID]
         slots = slots[:self.batch]
         if len(slots) < self.batch:
             raise RuntimeError('demod_isolated: %d decoded reads cached, %d needed' % (len(slots), self.batch))
-        ms = self.ctx.demod_isolated(slots, iters)
-        self._reset_cache()
-        return len(slots), ms
+        try:
+            ms = [self.ctx.demod_isolated(slots, iters, v) for v in variants]
+        finally:
+            self._reset_cache()
+        return len(slots), (ms[0] if len(ms) == 1 else ms)
 
     # ---- reference control flow --------------------------------------------------
     def _get(self, readsample, mtf, audio_offset):

@@ -21,7 +21,7 @@ MAX_VSYNCS = 16
 EXPORTS = ['ldg_create', 'ldg_destroy', 'ldg_last_error', 'ldg_set_filters', 'ldg_set_capture',
            'ldg_decode_reads', 'ldg_field_audio', 'ldg_assemble_frames', 'ldg_debug_read',
            'ldg_comb_ntsc', 'ldg_comb_reset', 'ldg_version', 'ldg_device_count', 'ldg_profile_enable',
-           'ldg_profile_read', 'ldg_synth_capture', 'ldg_capture_download', 'ldg_comb_ntsc_async', 'ldg_sync', 'ldg_demod_isolated', 'ldg_comb_set_opts', 'ldg_output_async', 'ldg_output_wait',
+           'ldg_profile_read', 'ldg_synth_capture', 'ldg_capture_download', 'ldg_comb_ntsc_async', 'ldg_sync', 'ldg_demod_isolated', 'ldg_demod_isolated_ex', 'ldg_comb_set_opts', 'ldg_output_async', 'ldg_output_wait',
            'ldg_host_alloc', 'ldg_host_free',
            'ldg_archive_fields', 'ldg_archive_audio', 'ldg_decode_reads_async', 'ldg_decode_reads_async2',
            'ldg_set_video_cut', 'ldg_decode_reads_wait',
@@ -133,6 +133,7 @@ def load(path=None):
     lib.ldg_archive_audio.argtypes = [vp, C.c_int, vp, vp, vp, C.c_int64, vp, vp]
     lib.ldg_sync.argtypes = [vp]
     lib.ldg_demod_isolated.argtypes = [vp, C.c_int, vp, C.c_int, C.POINTER(C.c_double)]
+    lib.ldg_demod_isolated_ex.argtypes = [vp, C.c_int, vp, C.c_int, C.c_int, C.POINTER(C.c_double)]
     lib.ldg_profile_enable.argtypes = [vp, C.c_int]
     lib.ldg_profile_read.argtypes = [vp, C.POINTER(KernelStat), C.c_int]
     lib.ldg_profile_spans.argtypes = [vp, C.POINTER(C.c_double), C.POINTER(C.c_int64)]
@@ -438,12 +439,13 @@ class Context:
         its first n device frames, on the comb stream."""
         self._check(self.lib.ldg_comb_async(self.h, n), 'ldg_comb_async')
 
-    def demod_isolated(self, slots, iters):
-        """Mean HIP-event ms of one demod-only launch (ldg_k_demod_iso) over these live slots."""
+    def demod_isolated(self, slots, iters, variant=0):
+        """Mean HIP-event ms of one demod-only launch over these live slots: variant 0
+        ldg_k_demod_iso (every block in full), 1 ldg_k_demod_iso_cut (the shipped body)."""
         sl = np.ascontiguousarray(slots, dtype=np.int32)
         ms = C.c_double()
-        self._check(self.lib.ldg_demod_isolated(self.h, sl.size, sl.ctypes.data, iters, C.byref(ms)),
-                    'ldg_demod_isolated')
+        self._check(self.lib.ldg_demod_isolated_ex(self.h, sl.size, sl.ctypes.data, iters, variant, C.byref(ms)),
+                    'ldg_demod_isolated_ex')
         return ms.value
 
     def output_async(self, tops, bottoms, tbc, rgb=None):

@@ -11,7 +11,8 @@ are fabric-side L2 request counters (Infinity-Cache hits included), so the
 figure is an upper estimate of DRAM bytes.
 
 SQ counters are summed over the chip per dispatch; per launch means are
-reported, and for the isolated demod (ldg_k_demod_iso) the derived figures:
+reported, and for the isolated demod (ldg_k_demod_iso, ldg_k_demod_iso_cut: the
+shipped body) and the pipeline's ldg_k_demod the derived figures:
   issue mix       ACTIVE_INST_{LDS,VALU,ANY} and WAIT_{ANY,INST_ANY} / WAVE_CYCLES
   LDS array busy  LDS_IDX_ACTIVE / BUSY_CU_CYCLES (both per-CU cycle sums)
   bank conflicts  LDS_BANK_CONFLICT / LDS_IDX_ACTIVE (extra cycles per array cycle)
@@ -94,14 +95,14 @@ def main(src, dst_prefix, *sq_srcs):
         rows.append((short(k)[:40], fetch, write, 2 * fetch + write))
     res = {'unit': 'bytes per launch (2*FETCH_SIZE + WRITE_SIZE)', 'source': src, 'kernels': out}
     for k, c in cs.items():
-        if short(k) in ('demod_iso', 'demod') and any(x.startswith('SQ_') for x in c):
+        if short(k) in ('demod_iso', 'demod_iso_cut', 'demod') and any(x.startswith('SQ_') for x in c):
             res[short(k) + '_sq'] = {'per_launch': {x: v for x, v in sorted(c.items())}, 'derived': derived(c)}
     json.dump(res, open(dst_prefix + '_pmc_traffic.json', 'w'), indent=1, sort_keys=True)
     with open(dst_prefix + '_pmc_traffic.txt', 'w') as fh:
         fh.write('%-40s %14s %14s %14s\n' % ('kernel', 'FETCH B', 'WRITE B', '2F+W B'))
         for r in sorted(rows, key=lambda r: -r[3]):
             fh.write('%-40s %14.0f %14.0f %14.0f\n' % r)
-        for name in ('demod_iso_sq', 'demod_sq'):
+        for name in ('demod_iso_sq', 'demod_iso_cut_sq', 'demod_sq'):
             if name in res:
                 fh.write('\n%s (per launch)\n' % name)
                 for x, v in res[name]['per_launch'].items():
