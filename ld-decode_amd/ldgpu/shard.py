@@ -418,7 +418,9 @@ class ShardedDecode:
 
     def finish(self, summaries):
         """Phase 2: exact audio from the archive and global frame indices.
-        Returns [(global_index, pcm int16, meta)] for this rank's frames."""
+        Returns [(global_index, pcm int16, meta)] for this rank's output frames (those
+        under the decode's frame limit); each pcm is a view of one array holding the
+        rank's audio in frame order."""
         dec = self.dec
         lp = dec.sysp.line_period
         o0 = start_offsets(summaries, lp, self.init['audio_offset'] if self.init else 0.0)[self.rank]
@@ -426,25 +428,24 @@ class ShardedDecode:
         offs = replay_offsets(o0, me['transitions'], lp)
         base = frame_offsets(summaries)[self.rank]
         frame0 = self.init['frame0'] if self.init else 0
-        ents = [(e, offs[t - me['t0']]) for f in dec.shard_frames for e, t in f['audio']]
-        pcm_by_entry = {}
+        frames = dec.shard_frames[:max(0, min(len(dec.shard_frames), self.limit - base))]
+        ents = [e for f in frames for e, _ in f['audio']]
+        eoff = [offs[t - me['t0']] for f in frames for _, t in f['audio']]
+        flat, lens = [], []
         step = dec.capacity
         for i in range(0, len(ents), step):
-            chunk = ents[i:i + step]
-            pcm, counts, _ = dec.ctx.archive_audio([e for e, _ in chunk], [o for _, o in chunk])
-            for j, (e, _) in enumerate(chunk):
-                if counts[j] < 0:
-                    raise RuntimeError('audio index error (reference: field invalid)')
-                pcm_by_entry[e] = pcm[j, :2 * counts[j]]
-        out = []
-        for i, f in enumerate(dec.shard_frames):
-            if base + i >= self.limit:
-                break
-            parts = [pcm_by_entry[e] for e, _ in f['audio']]
-            audio = np.concatenate(parts) if parts else np.zeros(0, dtype=np.int16)
-            meta = {'frame': frame0 + base + i, 'vbi': f['vbi'], 'nextsample': f['nextsample'], 'fields': f['fields']}
-            out.append((base + i, audio, meta))
-        return out
+            pcm, counts, _ = dec.ctx.archive_audio(ents[i:i + step], eoff[i:i + step])
+            if (counts < 0).any():
+                raise RuntimeError('audio index error (reference: field invalid)')
+            n2 = 2 * counts.astype(np.int64)
+            flat.append(pcm[np.arange(pcm.shape[1]) < n2[:, None]])    # row-major: entry by entry
+            lens.append(n2)
+        flat = np.concatenate(flat) if flat else np.zeros(0, dtype=np.int16)
+        ecum = np.concatenate([[0], np.cumsum(np.concatenate(lens))]) if lens else np.zeros(1, dtype=np.int64)
+        fb = ecum[np.cumsum([0] + [len(f['audio']) for f in frames])].tolist()   # frame k: flat[fb[k]:fb[k+1]]
+        return [(base + i, flat[fb[i]:fb[i + 1]],
+                 {'frame': frame0 + base + i, 'vbi': f['vbi'], 'nextsample': f['nextsample'], 'fields': f['fields']})
+                for i, f in enumerate(frames)]
 
     def end_state(self, summaries, comb_a0=None, line0=None):
         """The exact chain state after the last frame the decode outputs (frame limit - 1,
