@@ -233,6 +233,30 @@ def bound_analysis(sq, traffic, iso_ms, name='demod_iso_sq'):
     return out
 
 
+def demod_issue_lag(tab):
+    """Was the host on the demod's critical path?  tab: the timed steps' demod launches in
+    issue order (start, end, host issue; ms on the device clock, ldg_profile_span_table).
+    For each launch after the first, against the latest end of the launches issued before
+    it: gap = its start - that end (> 0: no demod was executing, the demod pipeline ran
+    dry) and late = its host issue - that end (> 0: the host had not issued it yet).  A
+    launch is host-late when both are positive: the GPU waited on the host."""
+    ok = ~np.isnan(tab[:, 0]) if len(tab) else np.zeros(0, bool)
+    tab = tab[ok]
+    if len(tab) < 2:
+        return None
+    prev_end = np.maximum.accumulate(tab[:-1, 1])
+    gap = tab[1:, 0] - prev_end
+    late = tab[1:, 2] - prev_end
+    idle = gap > 0.005
+    hl = idle & (late > 0)
+    return {'launches': int(len(gap)), 'idle_gaps': int(idle.sum()), 'host_late': int(hl.sum()),
+            'host_late_frac': round(float(hl.mean()), 4), 'idle_ms': round(float(gap[idle].sum()), 3),
+            'host_late_ms': round(float(np.minimum(gap, late)[hl].sum()), 3),
+            'median_gap_ms': round(float(np.median(gap)), 4),
+            'note': 'timed steps\' demod launches, issue order; gap = start - latest earlier end, late = host issue '
+                    '(steady clock mapped onto the device clock) - that end; host-late: gap > 5 us and late > 0'}
+
+
 def progress(rank, what):
     """a heartbeat on stderr (the JSON line stays the only stdout output)"""
     print('[bench rank %d] %s' % (rank, what), file=sys.stderr, flush=True)
@@ -428,8 +452,28 @@ class PALWorkload:
         self.args, self.dec = args, dec
         self.nsamp = int(40e6 * (args.seconds or 10.0))
         t0 = time.perf_counter()
-        self.raw = np.frombuffer(make_capture(self.nsamp, 'u8', system='PAL', clv=True, first_frame=3000,
-                                              seed=20181018 + rank), np.uint8)
+        seed = 20181018 + rank
+        # LDG_SYNTH_CACHE=<dir>: keep the host-synthesised capture between runs of a sweep
+        cache = os.environ.get('LDG_SYNTH_CACHE')
+        path = os.path.join(cache, 'pal_clv_u8_%d_%d.raw' % (self.nsamp, seed)) if cache else None
+        if path and os.path.exists(path):
+            self.raw = np.fromfile(path, dtype=np.uint8)
+        else:
+            import threading
+            done = threading.Event()
+
+            def beat():                          # the host synthesis is slow: heartbeats on stderr
+                while not done.wait(30.0):
+                    progress(rank, 'synthesising PAL capture (%.0f s)' % (time.perf_counter() - t0))
+            threading.Thread(target=beat, daemon=True).start()
+            try:
+                self.raw = np.frombuffer(make_capture(self.nsamp, 'u8', system='PAL', clv=True, first_frame=3000,
+                                                      seed=seed), np.uint8)
+            finally:
+                done.set()
+            if path:
+                os.makedirs(cache, exist_ok=True)
+                self.raw.tofile(path)
         dec.set_capture(self.raw, 0)
         self.synth_s = time.perf_counter() - t0
         self.scaling, self.fmt, self.system = 'weak', 0, 'PAL'
@@ -513,11 +557,16 @@ def main():
     stats = dec.ctx.profile_stats()
     if dec.htrace is not None:                 # LDG_HOSTTRACE=<file>: the host timeline of the timed steps
         with open(os.environ['LDG_HOSTTRACE'], 'w') as f:
+            f.write('# t0_ms %.4f (time.perf_counter() * 1e3 at the timed region\'s start)\n' % (t0 * 1e3))
             for t, ev, n in dec.htrace:
                 if t >= t0:
                     f.write('%.4f %s %d\n' % ((t - t0) * 1e3, ev, n))
     spans = dec.ctx.profile_spans()        # (launches, total ms) of the demod's execution spans
     busy = dec.ctx.profile_spans_union()   # (launches, ms with at least one demod executing)
+    span_tab = dec.ctx.profile_span_table()
+    issue = demod_issue_lag(span_tab)
+    if os.environ.get('LDG_SPANTABLE'):        # per-launch (start, end, issue, host issue) for timeline tools
+        np.savetxt(os.environ['LDG_SPANTABLE'], span_tab, fmt='%.4f')
     dec.ctx.profile(False)
     # the roofline leg: the demod alone (kernel ldg_k_demod_iso) over one full-width launch's
     # reads, ISO_ITERS launches back to back, HIP events on its stream -- the per-dispatch
@@ -654,7 +703,7 @@ def main():
                        park_redo=dec.stats.get('migrated', 0),
                        host_s={k: round(dec.stats.get(k, 0.0), 4)
                                for k in ('plan_s', 'gpu_s', 'replay_s', 'flush_s', 'wait_s')},
-                       inflight_at_wait=dec.stats.get('inflight_at_wait')),
+                       inflight_at_wait=dec.stats.get('inflight_at_wait'), demod_issue=issue),
     }
     if world > 1:
         line['per_rank_value'] = round(msps / world, 3)

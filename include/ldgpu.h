@@ -341,6 +341,13 @@ int ldg_profile_spans(ldg_ctx* ctx, double* total_ms, int64_t* count);
 /* The union of those spans (time with at least one demod launch executing; two
  * demod streams overlap consecutive launches) and the launch count. */
 int ldg_profile_spans_union(ldg_ctx* ctx, double* union_ms, int64_t* count);
+/* Every profiled demod launch in issue order, four doubles each: execution start,
+ * end, and the host's issue time, in ms on the device's constant-rate clock from
+ * the first launch's start (issue times mapped by a calibration taken in
+ * ldg_profile_enable, a few microseconds uncertain; NaN start / end for a launch
+ * that ran no workgroup), then the issue time in ms on the host's monotonic clock.
+ * Returns the number of rows written (<= max) or < 0. */
+int ldg_profile_span_table(ldg_ctx* ctx, double* out, int max);
 
 /* Benchmark roofline leg (not a reference interface): the demod kernel alone
  * (symbol ldg_k_demod_iso, so a kernel trace separates it from the pipeline's

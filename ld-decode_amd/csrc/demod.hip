@@ -879,6 +879,12 @@ extern "C" __global__ __launch_bounds__(1024) void ldg_k_audio2(
   }
 }
 
+// Profiling: the device's constant-rate clock, read once (ldg_profile_enable's
+// host-to-device clock calibration; out zeroed beforehand).
+extern "C" __global__ void ldg_k_clock(unsigned long long* out) {
+  if (threadIdx.x == 0) atomicMax(out, (unsigned long long)__builtin_amdgcn_s_memrealtime());
+}
+
 // RF filter table for one mtf level: RFVideo * MTF**m (lddecode_core.py:290-293).
 // m == 1 uses MTF itself (numpy's integer-power path); other m use
 // exp(m*log|MTF|) * cis(m*arg MTF) (cpow = cexp(m*clog)).  m == 0: RFVideo.

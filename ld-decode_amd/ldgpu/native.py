@@ -25,7 +25,7 @@ EXPORTS = ['ldg_create', 'ldg_destroy', 'ldg_last_error', 'ldg_set_filters', 'ld
            'ldg_host_alloc', 'ldg_host_free',
            'ldg_archive_fields', 'ldg_archive_audio', 'ldg_decode_reads_async', 'ldg_decode_reads_async2',
            'ldg_set_video_cut', 'ldg_decode_reads_wait',
-           'ldg_field_audio_async', 'ldg_field_audio_collect', 'ldg_comb_ntsc3d', 'ldg_cx_create', 'ldg_cx_destroy', 'ldg_cx_process', 'ldg_comb_pal', 'ldg_comb_set_state', 'ldg_profile_spans', 'ldg_profile_spans_union',
+           'ldg_field_audio_async', 'ldg_field_audio_collect', 'ldg_comb_ntsc3d', 'ldg_cx_create', 'ldg_cx_destroy', 'ldg_cx_process', 'ldg_comb_pal', 'ldg_comb_set_state', 'ldg_profile_spans', 'ldg_profile_spans_union', 'ldg_profile_span_table',
            'ldg_audio_offsets', 'ldg_comb_async', 'ldg_debug_rf_table']
 
 
@@ -138,6 +138,7 @@ def load(path=None):
     lib.ldg_profile_read.argtypes = [vp, C.POINTER(KernelStat), C.c_int]
     lib.ldg_profile_spans.argtypes = [vp, C.POINTER(C.c_double), C.POINTER(C.c_int64)]
     lib.ldg_profile_spans_union.argtypes = [vp, C.POINTER(C.c_double), C.POINTER(C.c_int64)]
+    lib.ldg_profile_span_table.argtypes = [vp, vp, C.c_int]
     lib.ldg_synth_capture.argtypes = [vp, C.POINTER(SynthParams), C.POINTER(C.c_double), C.POINTER(C.c_double),
                                       C.POINTER(C.c_uint32), C.c_int64]
     lib.ldg_capture_download.argtypes = [vp, vp, C.c_int64, C.c_int64]
@@ -504,6 +505,16 @@ class Context:
         t, n = C.c_double(0), C.c_int64(0)
         self._check(self.lib.ldg_profile_spans_union(self.h, C.byref(t), C.byref(n)), 'ldg_profile_spans_union')
         return int(n.value), float(t.value)
+
+    def profile_span_table(self):
+        """float64[n, 4]: every profiled demod launch in issue order -- execution start, end
+        and host issue time, ms on the device clock from the first start, and the issue time
+        in ms of the host's monotonic clock (time.perf_counter() * 1e3; ldg_profile_span_table)."""
+        out = np.zeros((8192, 4), dtype=np.float64)
+        n = self.lib.ldg_profile_span_table(self.h, out.ctypes.data, out.shape[0])
+        if n < 0:
+            self._check(n, 'ldg_profile_span_table')
+        return out[:n]
 
     def profile_stats(self):
         arr = (KernelStat * 64)()
