@@ -100,6 +100,9 @@ typedef struct ldg_field_info {
   int32_t log_flags;    /* what the reference prints while building this Field:
                          * bit q (q < 16): "vsync vote needed q"    lddecode_core.py:620
                          * LDG_LOG_NO_VSYNC: "no/corrupt VSYNC found, jumping forward"  :918 */
+  int32_t pad_;
+  int64_t readsample;   /* the read's start: the requested one, or where a start probe moved it
+                         * (ldg_decode_reads_async2, LDG_READ_PROBE) */
 } ldg_field_info;
 
 #define LDG_LOG_NO_VSYNC (1 << 16)
@@ -176,7 +179,16 @@ int ldg_decode_reads(ldg_ctx* ctx, int n, const int64_t* read_starts, const doub
  * can replay and output one batch while the next two decode. */
 int ldg_decode_reads_async(ldg_ctx* ctx, int n, const int64_t* read_starts, const double* mtf,
                            const int32_t* slots);
-/* The same with full[i] != 0 (full may be NULL) exempting read i from the video cut. */
+/* The same with per-read flags (full may be NULL):
+ *   LDG_READ_FULL  exempts read i from the video cut;
+ *   LDG_READ_PROBE marks read_starts[i] as a prediction: a probe demodulates the one
+ *     block centred on it and moves the read to the sync peak it finds within
+ *     0.3 lines (the start the previous field's nextfieldoffset gives when the
+ *     prediction is a sample or two off).  The read's actual start comes back in
+ *     its record (ldg_field_info.readsample).  Speculative planning only: the
+ *     caller still accepts a read only at the exact start its chain reaches. */
+#define LDG_READ_FULL 1
+#define LDG_READ_PROBE 2
 int ldg_decode_reads_async2(ldg_ctx* ctx, int n, const int64_t* read_starts, const double* mtf,
                             const int32_t* slots, const uint8_t* full);
 /* Video cut (0, the default: none): the demod of later decodes stops each block whose

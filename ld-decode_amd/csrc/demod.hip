@@ -333,7 +333,9 @@ __device__ unsigned long long g_stamps[LDG_STAMP_BLOCKS][32];
       vread_stride, vchan_stride, audio1, aread_stride, achan_stride, status, ospill, park_epoch, stiles, aslice,  \
       sst, sbits,                                                                                                 \
       bst, span
-template <bool CUT>
+// PROBE: one workgroup per probe read (slot smap[blockIdx.x], its block 0 only):
+// ldg_k_demod_probe, below.
+template <bool CUT, bool PROBE = false>
 __device__ __forceinline__ void demod_body(LDG_DEMOD_PARAMS) {
   __shared__ double2 s_x[M];          // 128 KiB: the 8192-point transforms
   __shared__ uint16_t s_bits[BLOCKLEN / 16];   // sync detector bits
@@ -349,8 +351,8 @@ __device__ __forceinline__ void demod_body(LDG_DEMOD_PARAMS) {
   // profiling: the launch's execution span on the constant-rate clock (first
   // workgroup start, last workgroup end), what a kernel trace reports
   if (span && tid == 0) atomicMax(&span[0], ~(unsigned long long)__builtin_amdgcn_s_memrealtime());
-  const int slot = smap[blockIdx.x / MAX_BLOCKS_PER_READ];
-  const int b = blockIdx.x % MAX_BLOCKS_PER_READ;
+  const int slot = PROBE ? smap[blockIdx.x] : smap[blockIdx.x / MAX_BLOCKS_PER_READ];
+  const int b = PROBE ? 0 : blockIdx.x % MAX_BLOCKS_PER_READ;
   const ReadDesc rd = reads[slot];
   if (b >= rd.n_blocks) return;
 
@@ -725,6 +727,77 @@ extern "C" __global__ __launch_bounds__(1024) void ldg_k_demod(LDG_DEMOD_PARAMS)
 extern "C" __global__ __launch_bounds__(1024) void ldg_k_demod_iso(LDG_DEMOD_PARAMS) { demod_body<false>(LDG_DEMOD_ARGS); }
 // The shipped body (video cut) for the same leg: ldg_demod_isolated_ex variant 1.
 extern "C" __global__ __launch_bounds__(1024) void ldg_k_demod_iso_cut(LDG_DEMOD_PARAMS) { demod_body<true>(LDG_DEMOD_ARGS); }
+
+// ---------------------------------------------------------------------------
+// Read-start probes (speculative planning, not a reference stage).  A read's
+// start is the previous field's nextfieldoffset: the absolute position of one
+// sync peak, the argmax of demod_sync over a window of the previous read
+// (lddecode_core.py:497-516, 926, 1204).  The planner predicts starts it has
+// not decoded from the field period; on a capture whose sync peaks jitter by a
+// sample or two (PAL: the trailing edge of the 0.5 MHz video through the
+// -55..-25 IRE window falls on either side of a sample) those predictions miss
+// and the read is decoded again.  A probe demodulates the one overlap-save
+// block centred on a predicted start and takes the argmax of its demod_sync
+// over +-0.3 lines around it: the peak the previous read's walk finds there
+// (the peak is a sample position in the capture; other block alignments move
+// demod_sync by far less than the peak's margin over its neighbours).  The
+// read is then decoded from that start.  A probe can only change where a
+// speculative read starts: the replay accepts a read only at the exact start
+// the reference's chain reaches, so a wrong probe costs a decode, never a
+// result.
+constexpr int PROBE_C = BLOCKSTEP / 2;    // output index of the predicted start in the probe's block
+
+extern "C" __global__ __launch_bounds__(1024) void ldg_k_demod_probe(LDG_DEMOD_PARAMS) {
+  demod_body<true, true>(LDG_DEMOD_ARGS);
+}
+
+// One wave per probe: the argmax (first maximum) of the probe block's demod_sync
+// over [PROBE_C - halfwin, PROBE_C + halfwin]; if its level passes the reference's
+// peak test (> .2) the read in the same slot is moved to start there (its
+// geometry as ldg_decode_reads_async2 sets it up).  The slot's status returns to
+// 0: the probe's demod wrote into the read's own channels, which its full demod
+// rewrites before any field kernel reads them.
+extern "C" __global__ __launch_bounds__(64) void ldg_k_probe_pick(const int32_t* __restrict__ psm,
+                                                                 const ReadDesc* __restrict__ preads,
+                                                                 ReadDesc* __restrict__ reads,
+                                                                 int32_t* __restrict__ status,
+                                                                 const double* __restrict__ sst,
+                                                                 const uint32_t* __restrict__ sbits, SysConst C,
+                                                                 int halfwin) {
+  const int slot = psm[blockIdx.x];
+  const int lane = threadIdx.x;
+  const bool eof = status[slot] == FS_EOF;
+  const SyncSrc ds(sst, sbits, slot, C);
+  double best = -1.0;
+  int bi = 0x7fffffff;
+  if (!eof) {
+    for (int o = PROBE_C - halfwin + lane; o <= PROBE_C + halfwin; o += 64) {
+      const double v = ds[o];
+      if (v > best) { best = v; bi = o; }      // ascending o per lane: first maximum
+    }
+  }
+#pragma unroll
+  for (int m = 1; m < 64; m <<= 1) {
+    const double ov = __shfl_xor(best, m);
+    const int oi = __shfl_xor(bi, m);
+    if (ov > best || (ov == best && oi < bi)) { best = ov; bi = oi; }
+  }
+  if (lane == 0) {
+    if (!eof && best > 0.2) {
+      ReadDesc r = reads[slot];
+      const int64_t start = preads[slot].readsample + bi;
+      r.readsample = start;
+      r.end = start + READLEN + 1;
+      r.s0 = start > BLOCKCUT ? start - BLOCKCUT : 0;
+      r.n_out = (int32_t)(r.end - r.s0 + 1);
+      r.n_blocks = (int32_t)((r.end - r.s0 + BLOCKSTEP - 1) / BLOCKSTEP);
+      r.n_audio = (int32_t)((r.end - r.s0) / AUDIO_DIV1 + 1);
+      r.n_audio2 = r.n_audio / AUDIO_DIV2;
+      if (r.n_out <= MAX_NOUT && r.n_blocks <= MAX_BLOCKS_PER_READ) reads[slot] = r;
+    }
+    status[slot] = 0;
+  }
+}
 
 // ---------------------------------------------------------------------------
 // Audio phase 1 (lddecode_core.py:321-328): per overlap-save block, the two

@@ -226,6 +226,18 @@ class GPUDecoder:
         self.trace = None          # diagnostics: planner steps (tools/miss_probe.py)
         self.boot_wide = os.environ.get('LDG_BOOT_WIDE', '1') == '1'   # +6.5% on the 60 s bench (tools/bootwide_ab.sh)
         self.miss_drain = os.environ.get('LDG_MISS_DRAIN', '1') == '1'
+        # while a drain waits for the launch that holds the missed read, keep `depth`
+        # launches in flight, planned on from the miss (the GPU otherwise idles once
+        # the launches ahead of that one land)
+        self.drain_refill = os.environ.get('LDG_DRAIN_REFILL', '0') == '1'
+        # read-start probes (ldg_decode_reads_async2 READ_PROBE): reads whose start the
+        # plan predicted are moved on the GPU to the sync peak a one-block probe finds
+        # there, so a start that jitters by a sample or two still decodes at the exact
+        # start the replay will ask for
+        self.probe = os.environ.get('LDG_PROBE', '1' if self.sysp.name == 'PAL' else '0') == '1'
+        self.probe_win = int(0.3 * self.rf.linelen) if hasattr(self.rf, 'linelen') else 760
+        self._probe_starts = []            # sorted (start, mtf) of probed reads in flight
+        self.plan_guessed = set()
         self.grid_votes = int(os.environ.get('LDG_GRID_VOTES', '1'))   # _grid_next (1: the previous period's start)
         self.hist_len = max(16, self.grid_votes * P + 2)                  # valid field starts the planner keeps
         # Video cut (ldg_set_video_cut): a steady-state read starts ~10 peaks before its
@@ -294,6 +306,7 @@ class GPUDecoder:
 
     def _reset_cache(self):
         self.cache, self.hints, self._hint_keys = {}, {}, []
+        self._probe_starts = []
         self.plan_located = 0
         self.full_keys = set()             # reads that came back FS_VCUT (decoded again in full)
 
@@ -343,6 +356,7 @@ class GPUDecoder:
         so reads past that frame are never needed."""
         new, seen, chain = [], set(), []
         located, guessing = 0, False   # leading steps resolved by a decoded read (hit or hint)
+        self.plan_guessed = guessed = set()      # new keys whose start came from a prediction
         starts = list(hist)
         # the replay stops once the last read's fd.tell() + 1.05 frames passes the
         # file size (lddecode.py:89): plan at most the rest of that frame beyond it
@@ -360,9 +374,11 @@ class GPUDecoder:
                 steps += 1
                 key = (int(sample), cur_mtf)
                 hit = self.cache.get(key)
-                if hit is None and key not in seen and key not in self.inflight:
+                if hit is None and key not in seen and key not in self.inflight and not self._probe_covers(key):
                     seen.add(key)
                     new.append(key)
+                    if guessing:
+                        guessed.add(key)
                     if len(new) >= want:
                         self.plan_located = located
                         return new, chain
@@ -490,8 +506,19 @@ class GPUDecoder:
             raise RuntimeError('read cache full (capacity %d)' % self.capacity)
         slots = free[:len(keys)]
         t0 = time.perf_counter()
-        full = [k in self.full_keys for k in keys] if self.full_keys else None
+        probe = self.probe and bool(self.plan_guessed)
+        full = None
+        if self.full_keys or probe:
+            full = [(native.READ_FULL if k in self.full_keys else 0) |
+                    (native.READ_PROBE if probe and k in self.plan_guessed and k not in self.full_keys else 0)
+                    for k in keys]
         self.ctx.decode_reads_async([k[0] for k in keys], [k[1] for k in keys], slots, full)
+        if probe:
+            import bisect
+            for k, f in zip(keys, full):
+                if f & native.READ_PROBE:
+                    bisect.insort(self._probe_starts, k)
+                    self.stats['probes'] = self.stats.get('probes', 0) + 1
         self.stats['gpu_s'] += time.perf_counter() - t0
         if self.htrace is not None:
             self.htrace.append((t0, 'launch', len(keys)))
@@ -515,7 +542,18 @@ class GPUDecoder:
             self.htrace.append((time.perf_counter(), 'waited', len(keys)))
         self.inflight.difference_update(keys)
         import bisect
+        if self._probe_starts:
+            for k in keys:
+                i = bisect.bisect_left(self._probe_starts, k)
+                if i < len(self._probe_starts) and self._probe_starts[i] == k:
+                    del self._probe_starts[i]
         for k, sl, inf in zip(keys, slots, infos):
+            if inf.readsample != k[0]:
+                # its probe moved it: the read is the one at its actual start
+                self.stats['probe_moved'] = self.stats.get('probe_moved', 0) + 1
+                k = (int(inf.readsample), k[1])
+                if k in self.cache:
+                    continue                # decoded already (this slot stays free)
             if inf.status == native.FS_MIGRATED:
                 # the demod's park was overwritten under it (compute-wave save/restore on a
                 # shared GPU): the read is void and stays undecoded; the replay's miss decodes it again
@@ -535,6 +573,21 @@ class GPUDecoder:
             for s in self._hint_keys[:-2048]:
                 self.hints.pop(s, None)
             self._hint_keys = self._hint_keys[-2048:]
+
+    def _probe_covers(self, key):
+        """A probed read in flight will land on this start if it is the sync peak within
+        the probe's window of that read's predicted start (same MTF)."""
+        ps = self._probe_starts
+        if not ps:
+            return False
+        import bisect
+        w = self.probe_win
+        i = bisect.bisect_left(ps, (key[0] - w, float('-inf')))
+        while i < len(ps) and ps[i][0] <= key[0] + w:
+            if ps[i][1] == key[1]:
+                return True
+            i += 1
+        return False
 
     def _note_miss(self, key):
         """Diagnostics: how far the nearest decoded read was from the one the replay needed."""
@@ -930,9 +983,17 @@ class GPUDecoder:
             # the replay stopped at a read a newer launch holds: it cannot move before
             # that launch lands, so wait for it rather than plan further ahead (each such
             # plan pins another batch of cached reads; a long capture once filled the cache)
-            while self.miss_drain and missed is not None and missed in self.inflight and self.pending:
+            while (self.miss_drain and missed is not None and (missed in self.inflight or self._probe_covers(missed))
+                   and self.pending):
                 self.stats['drain_waits'] = self.stats.get('drain_waits', 0) + 1
                 self._launch_wait()
+                while (self.drain_refill and steady and (missed in self.inflight or self._probe_covers(missed))
+                       and len(self.pending) < depth):
+                    plan, chain = self._plan(nextsample, self.mtf_level, self.last_framenr, self.last_isclv,
+                                             done == 0, self.batch, hist, frames_left=num_frames - done + 2)
+                    if not plan or not self._launch_async(plan, set(chain)):
+                        break
+                    self.stats['drain_refills'] = self.stats.get('drain_refills', 0) + 1
         return done
 
     def _flush(self, frames, W, H, sink):

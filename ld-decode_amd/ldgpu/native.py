@@ -15,6 +15,7 @@ LIB_PATH = os.path.join(HERE, 'libldgpu.so')
 LDG_OK = 0
 FS_VALID, FS_NO_VSYNC, FS_SHORT, FS_LINELOCS, FS_TBC, FS_EOF, FS_CRASH, FS_PENDING, FS_MIGRATED, FS_VCUT = range(10)
 VBI_NONE = -2147483648
+READ_FULL, READ_PROBE = 1, 2            # ldg_decode_reads_async2 per-read flags (include/ldgpu.h)
 LOG_NO_VSYNC = 1 << 16            # ldg_field_info.log_flags (include/ldgpu.h)
 MAX_VSYNCS = 16
 
@@ -37,7 +38,8 @@ class FieldInfo(C.Structure):
                 ('linecode', (C.c_int32 * 6) * 3), ('linecode_ok', C.c_int32 * 3),
                 ('vbi_minutes', C.c_int32), ('vbi_seconds', C.c_int32), ('vbi_clvframe', C.c_int32),
                 ('vbi_framenr', C.c_int32), ('vbi_status', C.c_int32), ('vbi_isclv', C.c_int32),
-                ('burst_group', C.c_int32), ('log_flags', C.c_int32)]
+                ('burst_group', C.c_int32), ('log_flags', C.c_int32), ('pad_', C.c_int32),
+                ('readsample', C.c_int64)]
 
 
 class Config(C.Structure):
@@ -293,9 +295,11 @@ class Context:
         return out
 
     def decode_reads_async(self, starts, mtfs, slots, full=None):
-        """Launch a decode (ldg_decode_reads_async2, up to 4 outstanding); decode_reads_wait()
-        returns the records of the oldest outstanding one.  full: per read, exempt it from the
-        video cut (set_video_cut; reads that came back FS_VCUT)."""
+        """Launch a decode (ldg_decode_reads_async2, up to 8 outstanding); decode_reads_wait()
+        returns the records of the oldest outstanding one.  full: per read flags, READ_FULL
+        (or True) exempts it from the video cut (set_video_cut; reads that came back FS_VCUT),
+        READ_PROBE moves a predicted start to the sync peak a probe finds (the record's
+        readsample is the start decoded)."""
         s, m, sl = (np.ascontiguousarray(starts, dtype=np.int64), np.ascontiguousarray(mtfs, dtype=np.float64),
                     np.ascontiguousarray(slots, dtype=np.int32))
         f = None if full is None else np.ascontiguousarray(full, dtype=np.uint8)

@@ -35,6 +35,17 @@ def nearest_field(s):
     return None
 
 
+def field_jitter(k):
+    """jitter='field': field k's start as the chain finds it is off the grid by -2..2
+    samples, a property of the signal (PAL's sync peaks, profiles/r04_f_pal_chain.json):
+    every read of field k - 1 reports the same start, whatever its own start."""
+    return (k * 37) % 5 - 2
+
+
+def chain_start(k, jitter):
+    return field_start(k) + (field_jitter(k) if jitter == 'field' else 0)
+
+
 def model_read(s, nsamples, jitter):
     """(status, istop, nextfieldoffset, framenr, linecount) of a read starting at s."""
     if s + 1000001 + 16384 > nsamples:
@@ -46,7 +57,10 @@ def model_read(s, nsamples, jitter):
         while field_start(j) < s:
             j += 1
         return native.FS_NO_VSYNC, 0, field_start(j) - s, None, 0
-    nfo = field_start(k + 1) - s + (1 if jitter and (s % 7 == 3) else 0)
+    if jitter == 'field':
+        nfo = chain_start(k + 1, jitter) - s
+    else:
+        nfo = field_start(k + 1) - s + (1 if jitter and (s % 7 == 3) else 0)
     return native.FS_VALID, int(k % 2 == 0), nfo, 2 + k // 2, 263 if k % 2 == 0 else 262
 
 
@@ -60,6 +74,7 @@ class FakeCtx:
         self._pending = []
         self._audio = 0
         self.reads = []
+        self.probed = 0
 
     def set_filters(self, *a):
         pass
@@ -72,10 +87,18 @@ class FakeCtx:
         busy = {s for p in self._pending for s in p[0]}
         assert not busy.intersection(slots), 'slot reused while in flight'
         infos = []
-        for s in starts:
-            self.reads.append(int(s))
-            st, top, nfo, fnr, lc = model_read(int(s), self.nsamples, self.jitter)
+        for i, s in enumerate(starts):
+            s = int(s)
+            if full is not None and full[i] & native.READ_PROBE:
+                # the GPU's start probe: the sync peak (the chain's start) within 0.3 lines
+                j = nearest_field(s)
+                if j is not None and abs(chain_start(j, self.jitter) - s) <= 760:
+                    s = chain_start(j, self.jitter)
+                self.probed += 1
+            self.reads.append(s)
+            st, top, nfo, fnr, lc = model_read(s, self.nsamples, self.jitter)
             f = native.FieldInfo()
+            f.readsample = s
             f.status, f.istop, f.nextfieldoffset, f.linecount = st, top, nfo, lc
             f.npeaks, f.nvsync = (400, 2) if st == native.FS_VALID else (400, 1)
             for name in ('vbi_minutes', 'vbi_seconds', 'vbi_clvframe', 'vbi_status'):
@@ -162,12 +185,36 @@ def test_replay_matches_sequential_reference(monkeypatch, jitter, votes):
     assert all(b == a + 1 for a, b in zip(dec.frame_numbers, dec.frame_numbers[1:]))
 
 
-def test_long_decode_with_mispredictions(monkeypatch):
+@pytest.mark.parametrize('refill', ['0', '1'])
+def test_long_decode_with_mispredictions(monkeypatch, refill):
     """A long decode whose predictions are sometimes a sample off keeps going: the
     planner waits for the launch holding the read the replay stopped at instead of
     pinning the whole read cache with ever further reads (round-2 fix; before it,
-    240 s captures died with 'read cache full' after ~3000 frames)."""
+    240 s captures died with 'read cache full' after ~3000 frames).  With the drain
+    refill (LDG_DRAIN_REFILL=1) it keeps `depth` launches in flight meanwhile, still
+    within the cache."""
+    monkeypatch.setenv('LDG_DRAIN_REFILL', refill)
     dec, n, nsamples = run_decode(monkeypatch, 2500, batch=8, jitter=True)
     ref = reference_chain(nsamples)
     assert n == len(ref) and dec.frame_numbers == [f for f, _ in ref]
     assert dec.stats['reads'] < 1.3 * dec.stats['reads_used']
+
+
+@pytest.mark.parametrize('probe', ['0', '1'])
+def test_start_probes_follow_a_jittering_chain(monkeypatch, probe):
+    """Field starts off the period grid by a couple of samples (a property of the
+    signal): without probes every such prediction is decoded twice; with them
+    (LDG_PROBE=1, ldg_decode_reads_async2 READ_PROBE) the predicted reads move to the
+    chain's starts and nearly every read decoded is used -- and the frames are the
+    sequential reference chain's either way."""
+    monkeypatch.setenv('LDG_PROBE', probe)
+    dec, n, nsamples = run_decode(monkeypatch, 600, batch=16, jitter='field')
+    ref = reference_chain(nsamples)
+    assert n == len(ref) and dec.frame_numbers == [f for f, _ in ref]
+    assert dec.last_meta['nextsample'] == ref[-1][1]
+    ratio = dec.stats['reads'] / dec.stats['reads_used']
+    if probe == '1':
+        assert dec.ctx.probed > 0 and dec.stats.get('probe_moved', 0) > 0
+        assert ratio < 1.05, ratio
+    else:
+        assert ratio > 1.3, ratio
