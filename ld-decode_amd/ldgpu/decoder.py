@@ -234,7 +234,13 @@ class GPUDecoder:
         # plan predicted are moved on the GPU to the sync peak a one-block probe finds
         # there, so a start that jitters by a sample or two still decodes at the exact
         # start the replay will ask for
-        self.probe = os.environ.get('LDG_PROBE', '1' if self.sysp.name == 'PAL' else '0') == '1'
+        # LDG_PROBE: 1 always, 0 never, auto (NTSC default) once the decode has wasted more
+        # than 5% of its reads (+32): a capture whose predictions hold (the synthetic NTSC
+        # bench: 0.6% waste) saves the probes' ~2%, a jittering one gets them.  PAL
+        # (default 1): config 3's start-up wander, 1.29 -> 1.04 reads per read used
+        # (profiles/r05_o_probe_ab.txt)
+        self.probe_mode = os.environ.get('LDG_PROBE', '1' if self.sysp.name == 'PAL' else 'auto')
+        self.probe = self.probe_mode == '1'
         self.probe_win = int(0.3 * self.rf.linelen) if hasattr(self.rf, 'linelen') else 760
         self._probe_starts = []            # sorted (start, mtf) of probed reads in flight
         self.plan_guessed = set()
@@ -506,6 +512,8 @@ class GPUDecoder:
             raise RuntimeError('read cache full (capacity %d)' % self.capacity)
         slots = free[:len(keys)]
         t0 = time.perf_counter()
+        if self.probe_mode == 'auto' and not self.probe:
+            self.probe = self.stats['reads'] - self.stats['reads_used'] > 0.05 * self.stats['reads_used'] + 32
         probe = self.probe and bool(self.plan_guessed)
         full = None
         if self.full_keys or probe:

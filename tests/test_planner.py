@@ -176,6 +176,7 @@ def test_replay_matches_sequential_reference(monkeypatch, jitter, votes):
     """Batched speculative decode == the reference's sequential read chain (frames, numbers, end),
     with the planner's period prediction from the last period (votes 1) or voted over 8."""
     monkeypatch.setenv('LDG_GRID_VOTES', str(votes))
+    monkeypatch.setenv('LDG_PROBE', '0')
     dec, n, nsamples = run_decode(monkeypatch, 300, batch=16, jitter=jitter)
     ref = reference_chain(nsamples)
     assert n == len(ref)
@@ -200,7 +201,7 @@ def test_long_decode_with_mispredictions(monkeypatch, refill):
     assert dec.stats['reads'] < 1.3 * dec.stats['reads_used']
 
 
-@pytest.mark.parametrize('probe', ['0', '1'])
+@pytest.mark.parametrize('probe', ['0', '1', 'auto'])
 def test_start_probes_follow_a_jittering_chain(monkeypatch, probe):
     """Field starts off the period grid by a couple of samples (a property of the
     signal): without probes every such prediction is decoded twice; with them
@@ -216,5 +217,8 @@ def test_start_probes_follow_a_jittering_chain(monkeypatch, probe):
     if probe == '1':
         assert dec.ctx.probed > 0 and dec.stats.get('probe_moved', 0) > 0
         assert ratio < 1.05, ratio
+    elif probe == 'auto':
+        # off until the waste passes 5%, then on for the rest of the decode
+        assert dec.ctx.probed > 0 and ratio < 1.2, ratio
     else:
         assert ratio > 1.3, ratio
