@@ -234,9 +234,10 @@ class GPUDecoder:
         # plan predicted are moved on the GPU to the sync peak a one-block probe finds
         # there, so a start that jitters by a sample or two still decodes at the exact
         # start the replay will ask for
-        # LDG_PROBE: 1 always, 0 never, auto (NTSC default) once the decode has wasted more
-        # than 5% of its reads (+32): a capture whose predictions hold (the synthetic NTSC
-        # bench: 0.6% waste) saves the probes' ~2%, a jittering one gets them.  PAL
+        # LDG_PROBE: 1 always, 0 never, auto (NTSC default) once the replay has missed a
+        # read that a decoded read a few samples away stood in for (jitter, _note_miss) more
+        # than 3 times and for over 1% of the reads used: a capture whose predictions hold
+        # (the synthetic NTSC bench) saves the probes' ~2%, a jittering one gets them.  PAL
         # (default 1): config 3's start-up wander, 1.29 -> 1.04 reads per read used
         # (profiles/r05_o_probe_ab.txt)
         self.probe_mode = os.environ.get('LDG_PROBE', '1' if self.sysp.name == 'PAL' else 'auto')
@@ -513,7 +514,8 @@ class GPUDecoder:
         slots = free[:len(keys)]
         t0 = time.perf_counter()
         if self.probe_mode == 'auto' and not self.probe:
-            self.probe = self.stats['reads'] - self.stats['reads_used'] > 0.05 * self.stats['reads_used'] + 32
+            j = self.stats.get('jitter_misses', 0)
+            self.probe = j > 3 and j > 0.01 * self.stats['reads_used']
         probe = self.probe and bool(self.plan_guessed)
         full = None
         if self.full_keys or probe:
@@ -605,6 +607,9 @@ class GPUDecoder:
             d = s - key[0]
             if abs(d) <= 200000 and (best is None or abs(d) < abs(best[0])):
                 best = (d, m == key[1])
+        if best is not None and best[1] and 0 < abs(best[0]) <= self.probe_win:
+            # a read of this field was decoded a few samples off: the start jitters
+            self.stats['jitter_misses'] = self.stats.get('jitter_misses', 0) + 1
         h = self.stats.setdefault('miss_log', [])
         if len(h) < 64:
             h.append(best)
