@@ -282,13 +282,28 @@ def test_end_to_end_vs_golden(case, batch):
 
 
 @pytest.mark.parametrize('case', ['ntsc_cav_u8_mtf_0p3s', 'pal_cav_u8_mtf_0p3s', 'ntsc_cav_lds_0p15s'])
-def test_demod2_end_to_end_vs_golden(case, monkeypatch):
+def test_demod2_end_to_end_vs_golden(case):
     """The register-resident demod (demod2.hip, LDG_DEMOD2=1: 512-thread workgroups, claimed
     park slots, layout-ordered filter tables) gives the golden decode too: metadata exact,
-    .tbc +-1 LSB, .pcm bit-exact (NTSC and PAL, the MTF chain, a 10-bit format)."""
+    .tbc +-1 LSB, .pcm bit-exact (NTSC and PAL, the MTF chain, a 10-bit format).  It is
+    the variant library libldgpu_demod2.so (build.py), so the check runs in a child process
+    that loads it."""
+    import subprocess
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    root = os.path.dirname(here)
+    lib = os.path.join(root, 'ld-decode_amd', 'ldgpu', 'libldgpu_demod2.so')
+    assert os.path.exists(lib), 'build the variant: __graft_entry__.build()'
+    env = dict(os.environ, LDGPU_LIB=lib, LDG_DEMOD2='1',
+               PYTHONPATH=os.pathsep.join([os.path.join(root, 'ld-decode_amd'), root, here]))
+    r = subprocess.run([sys.executable, '-c', 'import test_gpu_parity as t; t.demod2_check(%r)' % case],
+                       cwd=here, env=env, timeout=240, capture_output=True, text=True)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+
+
+def demod2_check(case):
     from ldgpu.decoder import GPUDecoder
     from ldgpu.formats import NAME_TO_FMT
-    monkeypatch.setenv('LDG_DEMOD2', '1')
     data, gold, frames, pcm, meta = oracle_decode(case)
     c = gold['settings']
     dec = GPUDecoder(system=c['system'], batch=8)
