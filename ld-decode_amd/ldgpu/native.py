@@ -354,17 +354,20 @@ class Context:
         sl = np.ascontiguousarray(slots, dtype=np.int32)
         self._check(self.lib.ldg_archive_fields(self.h, sl.size, sl.ctypes.data, int(first)), 'ldg_archive_fields')
 
-    def archive_audio(self, entries, offsets):
-        """ldg_field_audio over archive entries -> (pcm[n, 2048], counts, next offsets)."""
+    def archive_audio(self, entries, offsets, packed=False):
+        """ldg_field_audio over archive entries -> (pcm[n, 2048], counts, next offsets); packed:
+        pcm is one flat array, the fields' 2 * counts samples one after another."""
         n = len(entries)
-        stride = 2048
-        pcm = np.zeros((max(n, 1), stride), dtype=np.int16)
+        stride = 0 if packed else 2048
+        pcm = np.empty(max(n, 1) * 2048, dtype=np.int16) if packed else np.zeros((max(n, 1), stride), dtype=np.int16)
         counts = np.zeros(max(n, 1), dtype=np.int32)
         nxt = np.zeros(max(n, 1), dtype=np.float64)
         e = np.ascontiguousarray(entries, dtype=np.int64)
         o = np.ascontiguousarray(offsets, dtype=np.float64)
         self._check(self.lib.ldg_archive_audio(self.h, n, e.ctypes.data, o.ctypes.data, pcm.ctypes.data, stride,
                                                counts.ctypes.data, nxt.ctypes.data), 'ldg_archive_audio')
+        if packed:
+            return pcm[:int(2 * np.maximum(counts[:n], 0).sum())], counts[:n], nxt[:n]
         return pcm[:n], counts[:n], nxt[:n]
 
     def assemble_frames_device(self, tops, bottoms):

@@ -434,12 +434,11 @@ class ShardedDecode:
         flat, lens = [], []
         step = dec.capacity
         for i in range(0, len(ents), step):
-            pcm, counts, _ = dec.ctx.archive_audio(ents[i:i + step], eoff[i:i + step])
+            pcm, counts, _ = dec.ctx.archive_audio(ents[i:i + step], eoff[i:i + step], packed=True)
             if (counts < 0).any():
                 raise RuntimeError('audio index error (reference: field invalid)')
-            n2 = 2 * counts.astype(np.int64)
-            flat.append(pcm[np.arange(pcm.shape[1]) < n2[:, None]])    # row-major: entry by entry
-            lens.append(n2)
+            flat.append(pcm)                  # the entries' samples one after another
+            lens.append(2 * counts.astype(np.int64))
         flat = np.concatenate(flat) if flat else np.zeros(0, dtype=np.int16)
         ecum = np.concatenate([[0], np.cumsum(np.concatenate(lens))]) if lens else np.zeros(1, dtype=np.int64)
         fb = ecum[np.cumsum([0] + [len(f['audio']) for f in frames])].tolist()   # frame k: flat[fb[k]:fb[k+1]]
