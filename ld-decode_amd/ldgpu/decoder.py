@@ -226,6 +226,11 @@ class GPUDecoder:
         self.trace = None          # diagnostics: planner steps (tools/miss_probe.py)
         self.boot_wide = os.environ.get('LDG_BOOT_WIDE', '1') == '1'   # +6.5% on the 60 s bench (tools/bootwide_ab.sh)
         self.miss_drain = os.environ.get('LDG_MISS_DRAIN', '1') == '1'
+        # _hint_ahead in the boot plans: PAL +6% on config 3 (one boot launch fewer); on the
+        # NTSC capture the boot reads' next starts are not the chain's and four wide
+        # launches were wasted per decode (-10%), so NTSC keeps the narrow boot launch
+        # (profiles/r05_zb_boot_ahead_ab.txt)
+        self.boot_ahead = os.environ.get('LDG_BOOT_AHEAD', '1' if self.sysp.name == 'PAL' else '0') == '1'
         # while a drain waits for the launch that holds the missed read, keep `depth`
         # launches in flight, planned on from the miss (the GPU otherwise idles once
         # the launches ahead of that one land)
@@ -342,6 +347,23 @@ class GPUDecoder:
         nx, inf = self.hints[best]
         return (best, nx, inf.status, inf.istop, inf.vbi_framenr, inf.nvsync, [tuple(inf.vsync[q]) for q in range(min(inf.nvsync, 3))])
 
+    def _hint_ahead(self, start):
+        """The next field start seen by a decoded read that starts inside the field starting
+        at `start` (after it by less than half a field; valid or short) and lands about one
+        field after it: a read anywhere before a field's vsync finds the same next field
+        (the boot launch's nominal-spacing guesses, tools/boot_probe.py: reads at 799,232 /
+        1,600,353 / 2,399,232 of the PAL bench capture report the chain's 1,311,073 /
+        2,109,793 / 2,911,072).  None if there is none."""
+        import bisect
+        ks, f = self._hint_keys, self.field_nom
+        i = bisect.bisect_right(ks, start + 4096)
+        while i < len(ks) and ks[i] < start + f // 2:
+            nx, inf = self.hints[ks[i]]
+            if inf.status in (native.FS_VALID, native.FS_SHORT) and 0.95 * f < nx - start < 1.05 * f:
+                return nx
+            i += 1
+        return None
+
     def _hint(self, start):
         """(next start, field info) of the decoded read nearest `start` within 4096 samples, or None.
 
@@ -421,6 +443,17 @@ class GPUDecoder:
                         istop = bool(hinfo.istop)
                         fnr = hinfo.vbi_framenr if hinfo.vbi_framenr != native.VBI_NONE else None
                         clv = bool(hinfo.vbi_isclv)
+                    elif (not guessing and self.boot_ahead and len(hist) < self.period + 2
+                          and (ha := self._hint_ahead(key[0])) is not None):
+                        # boot: a decoded read later in this field (one of the boot launch's
+                        # guesses at the nominal field spacing) already saw where the next
+                        # field starts
+                        located += 1
+                        nxt = ha
+                        valid = True
+                        istop = (not prev_top) if prev_top is not None else self.sysp.topfirst
+                        fnr = (fr + 1) if (fr is not None and not isclv) else None
+                        clv = isclv
                     else:
                         guessing = True
                         if h is not None:
@@ -516,7 +549,9 @@ class GPUDecoder:
         if self.probe_mode == 'auto' and not self.probe:
             j = self.stats.get('jitter_misses', 0)
             self.probe = j > 3 and j > 0.01 * self.stats['reads_used']
-        probe = self.probe and bool(self.plan_guessed)
+        # (not the very first launch: its guesses at the nominal field spacing are not near
+        # field starts, they only locate the first fields)
+        probe = self.probe and bool(self.plan_guessed) and bool(self._hint_keys)
         full = None
         if self.full_keys or probe:
             full = [(native.READ_FULL if k in self.full_keys else 0) |
