@@ -226,11 +226,14 @@ class GPUDecoder:
         self.trace = None          # diagnostics: planner steps (tools/miss_probe.py)
         self.boot_wide = os.environ.get('LDG_BOOT_WIDE', '1') == '1'   # +6.5% on the 60 s bench (tools/bootwide_ab.sh)
         self.miss_drain = os.environ.get('LDG_MISS_DRAIN', '1') == '1'
-        # _hint_ahead in the boot plans: PAL +6% on config 3 (one boot launch fewer); on the
-        # NTSC capture the boot reads' next starts are not the chain's and four wide
-        # launches were wasted per decode (-10%), so NTSC keeps the narrow boot launch
-        # (profiles/r05_zb_boot_ahead_ab.txt)
-        self.boot_ahead = os.environ.get('LDG_BOOT_AHEAD', '1' if self.sysp.name == 'PAL' else '0') == '1'
+        # LDG_BOOT_AHEAD=1: _hint_ahead in the boot plans, one narrow boot launch fewer.  The
+        # boot reads locate the next fields exactly, but they start mid-field and carry no
+        # VBI, so the first wide launches are planned at the initial MTF: right on a CLV
+        # disc (PAL config 3: +6%), wrong on a CAV one, whose MTF follows the frame number
+        # (NTSC config 2: four wide launches redone per decode, -10%;
+        # profiles/r05_zb_boot_ahead_ab.txt).  Off by default: the capture's disc type is
+        # not known at boot, and the loss on CAV outweighs the gain on CLV.
+        self.boot_ahead = os.environ.get('LDG_BOOT_AHEAD', '0') == '1'
         # while a drain waits for the launch that holds the missed read, keep `depth`
         # launches in flight, planned on from the miss (the GPU otherwise idles once
         # the launches ahead of that one land)
