@@ -1,5 +1,5 @@
-"""The decoder's first launches on a PAL capture (boot): each launch's read starts, and
-the first launch's records (status, next start).  GPU box: python tools/boot_probe.py"""
+"""The decoder's first launches (boot): each launch's read starts, and the first launches'
+records (start, status, next start, istop).  GPU box: python tools/boot_probe.py [PAL|NTSC]"""
 import os
 import sys
 
@@ -12,9 +12,14 @@ def main():
     from ldgpu import native
     from ldgpu.decoder import GPUDecoder
     from ldgpu.synth import make_capture
-    data = np.frombuffer(make_capture(int(40e6 * 1.0), 'u8', system='PAL', clv=True, first_frame=3000,
-                                      seed=20181018), np.uint8)
-    dec = GPUDecoder(system='PAL', batch=96)
+    system = sys.argv[1] if len(sys.argv) > 1 else 'PAL'
+    if system == 'PAL':
+        data = np.frombuffer(make_capture(int(40e6 * 1.0), 'u8', system='PAL', clv=True, first_frame=3000,
+                                          seed=20181018), np.uint8)
+    else:
+        data = np.frombuffer(make_capture(int(40e6 * 2.0), 'u8', system='NTSC', first_frame=1, seed=20181017),
+                             np.uint8)
+    dec = GPUDecoder(system=system, batch=96)
     dec.set_capture(data, 0)
     orig_async, orig_wait = dec.ctx.decode_reads_async, dec.ctx.decode_reads_wait
     launches = []
@@ -27,7 +32,7 @@ def main():
         infos = orig_wait()
         if len(launches) <= 3:
             print('records:', [(int(i.readsample), int(i.status), int(i.readsample + i.nextfieldoffset), int(i.istop))
-                               for i in infos][:12], flush=True)
+                               for i in infos][:10], flush=True)
         return infos
     dec.ctx.decode_reads_async, dec.ctx.decode_reads_wait = la, wa
     dec.decode(sink=None)
