@@ -218,7 +218,8 @@ int ldg_field_audio_collect(ldg_ctx* ctx, int16_t* pcm, int64_t pcm_stride, int3
  * computed after its read slot is reused -- once a shard learns its exact
  * starting audio time offset from the shards before it. */
 int ldg_archive_fields(ldg_ctx* ctx, int n, const int32_t* slots, int64_t first);
-/* ldg_field_audio over archive entries.  pcm_stride 0: the fields' samples packed one
+/* ldg_field_audio over archive entries (any number: more than max_reads run in one
+ * launch on buffers of their own).  pcm_stride 0: the fields' samples packed one
  * after another (pcm holds at least n * 2048 int16; field i's 2 * counts[i] samples
  * follow field i - 1's). */
 int ldg_archive_audio(ldg_ctx* ctx, int n, const int64_t* entries, const double* offsets, int16_t* pcm,

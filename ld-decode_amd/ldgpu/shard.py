@@ -432,7 +432,7 @@ class ShardedDecode:
         ents = [e for f in frames for e, _ in f['audio']]
         eoff = [offs[t - me['t0']] for f in frames for _, t in f['audio']]
         flat, lens = [], []
-        step = dec.capacity
+        step = max(len(ents), 1)          # one call: the library runs any number of entries at once
         for i in range(0, len(ents), step):
             pcm, counts, _ = dec.ctx.archive_audio(ents[i:i + step], eoff[i:i + step], packed=True)
             if (counts < 0).any():
