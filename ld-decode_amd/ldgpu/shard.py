@@ -37,7 +37,6 @@ capture buffers when every rank has its own GPU, gloo through host memory
 otherwise.  A read that still falls outside the window raises WindowMiss and
 the rank re-runs with the whole capture.
 """
-import collections.abc
 import tempfile
 
 import numpy as np
@@ -268,39 +267,6 @@ class FrameSpill:
             self.fh = None
 
 
-class FinishedFrames(collections.abc.Sequence):
-    """A rank's output frames after the finish phase: item i is (global index, pcm int16,
-    meta), the pcm a view of the rank's one audio array (computed in full by finish);
-    the tuples and metadata dicts are built when an item is read."""
-
-    def __init__(self, base, frame0, frames, flat, fb, wrap=None):
-        self.base, self.frame0, self.frames, self.flat, self.fb, self.wrap = base, frame0, frames, flat, fb, wrap
-
-    def __len__(self):
-        return len(self.frames)
-
-    def _item(self, i):
-        f = self.frames[i]
-        g = self.base + i
-        t = (g, self.flat[int(self.fb[i]):int(self.fb[i + 1])],
-             {'frame': self.frame0 + g, 'vbi': f['vbi'], 'nextsample': f['nextsample'], 'fields': f['fields']})
-        return self.wrap(t) if self.wrap else t
-
-    def __getitem__(self, i):
-        if isinstance(i, slice):
-            return [self._item(k) for k in range(*i.indices(len(self)))]
-        if i < 0:
-            i += len(self)
-        if not 0 <= i < len(self):
-            raise IndexError(i)
-        return self._item(i)
-
-    def resident(self):
-        """the same frames as (global index, None, pcm, meta): frames left in HBM"""
-        return FinishedFrames(self.base, self.frame0, self.frames, self.flat, self.fb,
-                              lambda t: (t[0], None, t[1], t[2]))
-
-
 class ShardedDecode:
     """One rank's part of a field-group sharded decode, in two phases."""
 
@@ -475,8 +441,10 @@ class ShardedDecode:
             lens.append(2 * counts.astype(np.int64))
         flat = np.concatenate(flat) if flat else np.zeros(0, dtype=np.int16)
         ecum = np.concatenate([[0], np.cumsum(np.concatenate(lens))]) if lens else np.zeros(1, dtype=np.int64)
-        fb = ecum[np.cumsum([0] + [len(f['audio']) for f in frames])]   # frame k: flat[fb[k]:fb[k+1]]
-        return FinishedFrames(base, frame0, frames, flat, fb)
+        fb = ecum[np.cumsum([0] + [len(f['audio']) for f in frames])].tolist()   # frame k: flat[fb[k]:fb[k+1]]
+        return [(base + i, flat[fb[i]:fb[i + 1]],
+                 {'frame': frame0 + base + i, 'vbi': f['vbi'], 'nextsample': f['nextsample'], 'fields': f['fields']})
+                for i, f in enumerate(frames)]
 
     def end_state(self, summaries, comb_a0=None, line0=None):
         """The exact chain state after the last frame the decode outputs (frame limit - 1,
@@ -606,7 +574,7 @@ def _decode_sharded(dec, rank, world, allgather, sink, start_frame, length, star
         stats['extended_frames'] = stats.get('extended_frames', 0) + sd.extended
         stats['frames_total'] = sum(s['n'] for s in summ)
     if resident:
-        return res.resident()
+        return [(g, None, a, m) for (g, a, m) in res]
     if sd.rgb is not None:
         return [(g, pic, a, m, rgb) for (g, a, m), pic, rgb in zip(res, sd.frames, sd.rgb)]
     return [(g, pic, a, m) for (g, a, m), pic in zip(res, sd.frames)]
