@@ -104,3 +104,27 @@ def test_arange_last_matches_numpy():
         step = float(rng.uniform(1e-4, 1))
         stop = st + float(rng.uniform(step, 100 * step))
         assert arange_last(st, stop, step) == np.arange(st, stop, step)[-1]
+
+
+def _bench():
+    import importlib.util
+    import os
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    spec = importlib.util.spec_from_file_location('ldg_bench', os.path.join(root, 'bench.py'))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def test_demod_issue_lag_classifies_launches():
+    """bench.py checks.demod_issue: a launch is host-late when no demod was executing
+    before it started (gap > 5 us) and the host issued it after the last one ended."""
+    b = _bench()
+    # (start, end, host issue, host ms): #1 queued early (overlaps #0), #2 issued late into an
+    # idle GPU, #3 issued early but started after a gap (GPU-side), #4 a launch with no workgroup
+    tab = np.array([[0.0, 2.0, -1.0, 0.0], [1.5, 4.0, -0.5, 0.0], [4.3, 6.0, 4.2, 0.0],
+                    [6.4, 8.0, 3.0, 0.0], [np.nan, np.nan, 7.0, 0.0]])
+    r = b.demod_issue_lag(tab)
+    assert r['launches'] == 3 and r['idle_gaps'] == 2 and r['host_late'] == 1
+    assert abs(r['host_late_ms'] - 0.2) < 1e-9 and abs(r['idle_ms'] - 0.7) < 1e-9
+    assert b.demod_issue_lag(tab[:1]) is None
