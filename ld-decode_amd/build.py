@@ -75,9 +75,27 @@ def build_demod2(force=False, verbose=True):
 
 
 def build(force=False, verbose=True):
-    """Compile libldgpu.so (and the demod2 variant) unless up to date; always says which
-    (the driver's record shows whether this run compiled)."""
-    build_demod2(force, verbose)
+    """Compile libldgpu.so (and the demod2 variant, in parallel) unless up to date; always
+    says which (the driver's record shows whether this run compiled)."""
+    import threading
+    err = []
+
+    def variant():
+        try:
+            build_demod2(force, verbose)
+        except Exception as e:           # reported after the main library
+            err.append(e)
+    th = threading.Thread(target=variant)
+    th.start()
+    try:
+        return _build_main(force, verbose)
+    finally:
+        th.join()
+        if err:
+            raise err[0]
+
+
+def _build_main(force, verbose):
     if not force and up_to_date():
         if verbose:
             print('libldgpu.so up to date (sources sha256 %s): not recompiled' % source_hash()[:16], flush=True)
