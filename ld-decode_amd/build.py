@@ -17,7 +17,11 @@ FLAGS = ['--offload-arch=gfx950', '-O3', '-std=c++17', '-fPIC', '-shared',
          # the machine scheduler's max-ILP strategy (no kernel spills; the demod stays at
          # 121 VGPRs): 2-step bench -1.3% time in 3/3 interleaved rounds and -0.3% in 2/4, 20 sustained
          # steps -0.15% in 2/3 (profiles/r02_s84_*, r02_s85_*, r02_s91_*)
-         '-mllvm', '--amdgpu-sched-strategy=max-ilp']
+         '-mllvm', '--amdgpu-sched-strategy=max-ilp',
+         # s_setprio around each wave's memory bursts: 20-step bench +0.25 / +0.25 / +0.34%, the
+         # isolated demod -0.3 to -1.3% (6 of 6 A/B pairs, round 5; inside the run-to-run band but
+         # one-signed)
+         '-mllvm', '--amdgpu-set-wave-priority']
 
 
 def sources():
