@@ -47,6 +47,9 @@ CASES = {
     'ntsc_cav_u8_mtf0_0p3s': dict(seconds=0.3, fmt='u8', system='NTSC', kw={'seed': 12, 'first_frame': 9997}),
     # ... and a PAL CAV disc from picture ~1200 (the same chain on FieldPAL)
     'pal_cav_u8_mtf_0p3s': dict(seconds=0.3, fmt='u8', system='PAL', kw={'seed': 13, 'first_frame': 1200}),
+    # PAL through the 10-bit loaders (the demod's .lds / .r30 unpacking with PAL's geometry)
+    'pal_clv_lds_0p15s': dict(seconds=0.15, fmt='lds', system='PAL', kw={'clv': True, 'first_frame': 3000, 'seed': 14}),
+    'pal_cav_r30_0p15s': dict(seconds=0.15, fmt='r30', system='PAL', kw={'seed': 15}),
 }
 
 

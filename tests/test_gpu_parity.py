@@ -225,8 +225,10 @@ def test_pal_field_records_and_pilot_refine(decoded_pal):
 CASES = ['ntsc_cav_u8_0p2s', 'ntsc_clv_u8_0p2s', 'ntsc_cav_r30_0p15s', 'ntsc_cav_lds_0p15s', 'pal_clv_u8_0p2s',
          'ntsc_cav_s16_0p15s', 'ntsc_cav_u8_mid_0p2s',
          # the MTF chain: a first frame re-read at MTF 0.88 (NTSC and PAL), the clamp to 0
-         'ntsc_cav_u8_mtf_0p3s', 'ntsc_cav_u8_mtf0_0p3s', 'pal_cav_u8_mtf_0p3s']
-MTF_CASES = CASES[-3:]
+         'ntsc_cav_u8_mtf_0p3s', 'ntsc_cav_u8_mtf0_0p3s', 'pal_cav_u8_mtf_0p3s',
+         # PAL through the 10-bit loaders
+         'pal_clv_lds_0p15s', 'pal_cav_r30_0p15s']
+MTF_CASES = ['ntsc_cav_u8_mtf_0p3s', 'ntsc_cav_u8_mtf0_0p3s', 'pal_cav_u8_mtf_0p3s']
 _ORACLE = {}
 
 

@@ -23,7 +23,7 @@ def load_case(case):
 
 
 @pytest.mark.parametrize('case', ['ntsc_cav_u8_0p2s', 'ntsc_clv_u8_0p2s', 'ntsc_cav_r30_0p15s', 'ntsc_cav_lds_0p15s',
-                                  'pal_clv_u8_0p2s',
+                                  'pal_clv_u8_0p2s', 'pal_clv_lds_0p15s',
                                   'ntsc_cav_s16_0p15s', 'ntsc_cav_u8_mid_0p2s'])
 def test_oracle_matches_golden(case):
     mg, gold = load_case(case)
