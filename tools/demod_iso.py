@@ -23,9 +23,18 @@ def main():
     dec.ctx.synth(n, fmt=0, first_frame=1, clv=False, seed=20181017)
     dec.use_resident_capture(0, n)
     t0 = time.perf_counter()
-    dec.decode(length=100)
-    t1 = time.perf_counter()
-    reads, ms = dec.demod_isolated(iters)
+    if os.environ.get('LDG_ISO_ANY') == '1':
+        # timing probes of deliberately broken builds: 96 reads at the nominal field
+        # spacing, decoded once (whatever their fields come out as), then the leg
+        starts = [1000000 + 667333 * k for k in range(96)]
+        dec.ctx.decode_reads_async(starts, [1.0] * 96, list(range(96)))
+        dec.ctx.decode_reads_wait()
+        t1 = time.perf_counter()
+        reads, ms = 96, dec.ctx.demod_isolated(list(range(96)), iters)
+    else:
+        dec.decode(length=100)
+        t1 = time.perf_counter()
+        reads, ms = dec.demod_isolated(iters)
     print(json.dumps({'reads': reads, 'iters': iters, 'ms_per_launch': round(ms, 4), 'decode_s': round(t1 - t0, 2),
                       'demod2': os.environ.get('LDG_DEMOD2', '0') != '0'}))
 
