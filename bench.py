@@ -47,6 +47,7 @@ HBM_PEAK_GBS = 8000.0
 FP64_PEAK_TFLOPS = 78.6                           # MI355X FP64 vector (spec)
 READ_BLOCKS = 66                                  # overlap-save blocks per 1e6-sample field read
 ISO_ITERS = 20                                    # launches of the isolated roofline leg
+ISO_READS = 96                                    # reads per isolated launch (rounds 1-5 quote 96-read launches)
 # the leg's kernels: ldg_k_demod_iso (full blocks) and ldg_k_demod_iso_cut (the shipped body);
 # the 512-thread demod (LDG_DEMOD2=1, experimental) has the first only
 ISO_VARIANTS = (0,) if os.environ.get('LDG_DEMOD2', '0') != '0' else (0, 1)
@@ -54,7 +55,7 @@ ISO_VARIANTS = (0,) if os.environ.get('LDG_DEMOD2', '0') != '0' else (0, 1)
 
 def iso_leg(dec):
     """(reads, full-body ms, shipped-body ms or None) of the isolated roofline leg"""
-    reads, ms = dec.demod_isolated(ISO_ITERS, ISO_VARIANTS)
+    reads, ms = dec.demod_isolated(ISO_ITERS, ISO_VARIANTS, reads=ISO_READS)
     return (reads, ms, None) if len(ISO_VARIANTS) == 1 else (reads, ms[0], ms[1])
 # the FFT flops the demod executes per block (5 N log2 N): six 8192-point complex transforms
 # (raw R2C, analytic even / odd, demod R2C, C2R 0.5 MHz, C2R video) + two 1024-point audio IFFTs;
@@ -73,10 +74,10 @@ def parse():
                     help='config 5: one 1 h NTSC CLV capture field-sharded across the ranks (default when N > 1)')
     ap.add_argument('--independent', action='store_true',
                     help='N > 1: each rank decodes its own capture (weak scaling) instead of the sharded config 5')
-    # reads per launch: over the driver's 20 sustained steps 96 beat 128 in 5 of 6 interleaved
-    # comparisons (-0.5..-0.9% time, profiles/r02_s92_s93_batch_20step.txt); in 2-step runs
-    # 128 had measured +1% (tools/batch_ab2.sh), before the clock settles
-    ap.add_argument('--batch', type=int, default=96)
+    # reads per launch: 128 since round 5 (probes): PAL +1.6% in 5 of 5 interleaved pairs, NTSC
+    # level at 20 steps and +0.6% at 2 (profiles/r05_zs_batch.txt, r05_zt_batch.txt); round 2 had
+    # 96 ahead by 0.5-0.9% (profiles/r02_s92_s93_batch_20step.txt), before the planner's hints
+    ap.add_argument('--batch', type=int, default=128)
     ap.add_argument('--fmt', type=int, default=0, help='capture format: 0 u8, 1 s16, 2 .r30, 3 .lds (10-bit packed)')
     ap.add_argument('--system', default='NTSC', choices=('NTSC', 'PAL'),
                     help='PAL: config 3 (PAL CLV 40 MSPS u8, host-synthesised, the PAL Y/C decoder)')

@@ -41,7 +41,7 @@ def parse(argv=None):
     p.add_argument('-c', '--cut', dest='cut', action='store_true', help='cut (to r16) instead of decode')
     # MI355X additions
     p.add_argument('--device', type=int, default=0, help='HIP device')
-    p.add_argument('--batch', type=int, default=96, help='field reads per GPU launch')
+    p.add_argument('--batch', type=int, default=128, help='field reads per GPU launch')
     p.add_argument('--comb', action='store_true',
                    help='also write <outfile>.rgb through the 2D NTSC comb (PAL: the build-defined PAL Y/C '
                         'decoder, 1057x576 rgb48)')

@@ -652,8 +652,8 @@ class GPUDecoder:
         if len(h) < 64:
             h.append(best)
 
-    def demod_isolated(self, iters=10, variants=(0,)):
-        """(reads, ms per launch) of the demod alone over `batch` decoded reads,
+    def demod_isolated(self, iters=10, variants=(0,), reads=None):
+        """(reads, ms per launch) of the demod alone over `reads` (default `batch`) decoded reads,
         `iters` launches back to back (the benchmark's roofline leg).  The reads are the
         most recent cached reads whose field decoded (FS_VALID): every block of such a
         read lies inside the resident capture, so each launch demodulates whole reads
@@ -663,9 +663,10 @@ class GPUDecoder:
         (native.Context.demod_isolated) run in turn over the same reads; with more than
         one the ms figure is a list in that order."""
         slots = [sl for sl, inf in reversed(list(self.cache.values())) if inf.status == native.FS_VALID]
-        slots = slots[:self.batch]
-        if len(slots) < self.batch:
-            raise RuntimeError('demod_isolated: %d decoded reads cached, %d needed' % (len(slots), self.batch))
+        want = self.batch if reads is None else min(int(reads), self.batch)
+        slots = slots[:want]
+        if len(slots) < want:
+            raise RuntimeError('demod_isolated: %d decoded reads cached, %d needed' % (len(slots), want))
         try:
             ms = [self.ctx.demod_isolated(slots, iters, v) for v in variants]
         finally:
