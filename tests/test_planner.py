@@ -222,3 +222,21 @@ def test_start_probes_follow_a_jittering_chain(monkeypatch, probe):
         assert dec.ctx.probed > 0 and ratio < 1.2, ratio
     else:
         assert ratio > 1.3, ratio
+
+
+def test_demod_isolated_read_count(monkeypatch):
+    """bench.py's roofline leg: `reads` picks how many decoded reads one isolated launch
+    demodulates (96 whatever the pipeline's batch), default the batch; too few refuse."""
+    monkeypatch.setenv('LDG_PROBE', '0')
+    dec, _, _ = run_decode(monkeypatch, 60, batch=16, jitter=False)
+    seen = []
+    monkeypatch.setattr(dec.ctx, 'demod_isolated', lambda slots, iters, v: seen.append(list(slots)) or 1.0,
+                        raising=False)
+    cached = dict(dec.cache)
+    assert dec.demod_isolated(3, reads=8) == (8, 1.0)
+    assert len(seen[-1]) == 8 and len(set(seen[-1])) == 8
+    dec.cache.update(cached)
+    assert dec.demod_isolated(3, (0, 1)) == (16, [1.0, 1.0])
+    assert [len(s) for s in seen[-2:]] == [16, 16]
+    with pytest.raises(RuntimeError):
+        dec.demod_isolated(3, reads=8)              # the read cache was dropped
