@@ -49,8 +49,7 @@ READ_BLOCKS = 66                                  # overlap-save blocks per 1e6-
 ISO_ITERS = 20                                    # launches of the isolated roofline leg
 ISO_READS = 96                                    # reads per isolated launch (rounds 1-5 quote 96-read launches)
 # the leg's kernels: ldg_k_demod_iso (full blocks) and ldg_k_demod_iso_cut (the shipped body);
-# the 512-thread demod (LDG_DEMOD2=1, experimental) has the first only
-ISO_VARIANTS = (0,) if os.environ.get('LDG_DEMOD2', '0') != '0' else (0, 1)
+ISO_VARIANTS = (0, 1)
 
 
 def iso_leg(dec):
@@ -628,17 +627,24 @@ def main():
     units_iso = iso_reads * samples_per_read
     achieved = bps * units_iso / (iso_ms * 1e-3) / 1e9
     traffic, lds, traffic_cut, lds_cut = None, None, None, None
-    # the committed --pmc passes of this system's bench command (PAL stores the pilot channel too)
+    # the committed --pmc passes of this system's bench command (PAL stores the pilot channel
+    # too), attached only when they were taken of this same library (its build's source hash)
+    from ldgpu.native import lib_source_hash
     pmc = os.path.join(ROOT, 'profiles', 'pmc_traffic_pal.json' if pal else 'pmc_traffic.json')
+    lib_hash = lib_source_hash()
+    counters = {'lib_source_sha256': lib_hash, 'pmc_file': 'profiles/' + os.path.basename(pmc), 'state': 'absent'}
     if os.path.exists(pmc):
-        try:
-            pj = json.load(open(pmc))
+        pj = json.load(open(pmc))
+        counters['pmc_lib_source_sha256'] = pj.get('lib_source_sha256')
+        if lib_hash is not None and pj.get('lib_source_sha256') == lib_hash:
+            counters['state'] = 'fresh'
             traffic = pj['kernels'].get('demod_iso')
             lds = bound_analysis(pj.get('demod_iso_sq'), traffic, iso_ms)
             traffic_cut = pj['kernels'].get('demod_iso_cut')
-            lds_cut = bound_analysis(pj.get('demod_iso_cut_sq'), traffic_cut, cut_ms, 'demod_iso_cut_sq')
-        except Exception:
-            traffic = traffic_cut = None
+            if cut_ms:
+                lds_cut = bound_analysis(pj.get('demod_iso_cut_sq'), traffic_cut, cut_ms, 'demod_iso_cut_sq')
+        else:
+            counters['state'] = 'stale'      # profiled from another build: not attached
     # the pipeline's own demod launches (co-running with the field kernels, two demod streams
     # overlapping consecutive launches): in-kernel execution spans and HIP-event intervals
     dom_launches, dom_ms = stats.get('demod', (1, float('nan')))
@@ -664,7 +670,7 @@ def main():
         'algorithmic_bytes_per_launch': round(bps * units_iso),
         'traffic_unit': 'bytes per launch, 2*FETCH_SIZE + WRITE_SIZE (profiles/%s, demod_iso)' % os.path.basename(pmc),
         'traffic_x_algorithmic': (traffic / (bps * units_iso)) if traffic else None,
-        'issue': lds, 'fp64': fp64,
+        'issue': lds, 'fp64': fp64, 'counters': counters,
         'production': {
             'kernel': 'ldg_k_demod_iso_cut: the shipped demod body (ldg_k_demod, video cut) under its own symbol, '
                       'same reads, launches and units as the leg above',

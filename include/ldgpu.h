@@ -171,7 +171,7 @@ int ldg_set_capture(ldg_ctx* ctx, const void* data, int64_t nsamples, int fmt, i
 int ldg_decode_reads(ldg_ctx* ctx, int n, const int64_t* read_starts, const double* mtf, const int32_t* slots,
                      ldg_field_info* info);
 /* The same in two halves: launch without waiting, then wait and fetch the
- * records of the OLDEST outstanding call.  Up to four calls may be outstanding:
+ * records of the OLDEST outstanding call.  Up to eight calls may be outstanding:
  * a call's demod overlaps the field kernels of the calls before it, and with
  * three outstanding the demods run back to back.  Slots of
  * outstanding calls must be distinct and are not readable until their wait.
@@ -179,18 +179,21 @@ int ldg_decode_reads(ldg_ctx* ctx, int n, const int64_t* read_starts, const doub
  * can replay and output one batch while the next two decode. */
 int ldg_decode_reads_async(ldg_ctx* ctx, int n, const int64_t* read_starts, const double* mtf,
                            const int32_t* slots);
-/* The same with per-read flags (full may be NULL):
+/* The same with per-read flags (full may be NULL; in/out):
  *   LDG_READ_FULL  exempts read i from the video cut;
  *   LDG_READ_PROBE marks read_starts[i] as a prediction: a probe demodulates the one
  *     block centred on it and moves the read to the sync peak it finds within
  *     0.3 lines (the start the previous field's nextfieldoffset gives when the
  *     prediction is a sample or two off).  The read's actual start comes back in
  *     its record (ldg_field_info.readsample).  Speculative planning only: the
- *     caller still accepts a read only at the exact start its chain reaches. */
+ *     caller still accepts a read only at the exact start its chain reaches.  On
+ *     return the flag is left set exactly for the reads that were probed (a probe
+ *     block outside the resident capture, or a stage-isolation run without the
+ *     demod, clears it): the caller tracks only those as probes in flight. */
 #define LDG_READ_FULL 1
 #define LDG_READ_PROBE 2
 int ldg_decode_reads_async2(ldg_ctx* ctx, int n, const int64_t* read_starts, const double* mtf,
-                            const int32_t* slots, const uint8_t* full);
+                            const int32_t* slots, uint8_t* full);
 /* Video cut (0, the default: none): the demod of later decodes stops each block whose
  * outputs start at or past `out_samples` (read output index: sample start - 1024) after
  * the sync channel -- the video, burst and pilot channels are not computed there.  A
@@ -373,7 +376,7 @@ int ldg_demod_isolated(ldg_ctx* ctx, int n, const int32_t* slots, int iters, dou
 /* The same leg by variant: 0 = ldg_k_demod_iso (as above, every block in full),
  * 1 = ldg_k_demod_iso_cut, the shipped body of ldg_k_demod (blocks past a read's
  * video cut stop after the sync channel) under its own symbol.  LDG_EINVAL for
- * other variants, and for 1 when the 512-thread demod (LDG_DEMOD2) is selected. */
+ * other variants. */
 int ldg_demod_isolated_ex(ldg_ctx* ctx, int n, const int32_t* slots, int iters, int variant, double* ms_per_launch);
 
 /* ---- benchmark / test tooling (not a reference interface) ----------------------

@@ -59,47 +59,9 @@ def build_variant(out, defines=(), verbose=True):
     return out
 
 
-# The experimental 512-thread demod (csrc/demod2.hip, LDG_DEMOD2=1) lives in a variant
-# library: its kernels in the default one moved ldg_k_demod's code and cost ~2%.
-DEMOD2 = os.path.join(HERE, 'ldgpu', 'libldgpu_demod2.so')
-
-
-def build_demod2(force=False, verbose=True):
-    stamp = DEMOD2 + '.sha256'
-    h = source_hash()
-    if not force and os.path.exists(DEMOD2) and os.path.exists(stamp) and open(stamp).read().strip() == h:
-        if verbose:
-            print('libldgpu_demod2.so up to date: not recompiled', flush=True)
-        return DEMOD2
-    build_variant(DEMOD2 + '.tmp', ('LDG_WITH_DEMOD2',), verbose)
-    os.replace(DEMOD2 + '.tmp', DEMOD2)
-    with open(stamp, 'w') as fh:
-        fh.write(h + '\n')
-    return DEMOD2
-
-
 def build(force=False, verbose=True):
-    """Compile libldgpu.so (and the demod2 variant, in parallel) unless up to date; always
-    says which (the driver's record shows whether this run compiled)."""
-    import threading
-    err = []
-
-    def variant():
-        try:
-            build_demod2(force, verbose)
-        except Exception as e:           # reported after the main library
-            err.append(e)
-    th = threading.Thread(target=variant)
-    th.start()
-    try:
-        return _build_main(force, verbose)
-    finally:
-        th.join()
-        if err:
-            raise err[0]
-
-
-def _build_main(force, verbose):
+    """Compile libldgpu.so unless up to date; always says which (the driver's record
+    shows whether this run compiled)."""
     if not force and up_to_date():
         if verbose:
             print('libldgpu.so up to date (sources sha256 %s): not recompiled' % source_hash()[:16], flush=True)

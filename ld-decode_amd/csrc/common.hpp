@@ -12,6 +12,10 @@ constexpr int BLOCKSTEP = BLOCKLEN - BLOCKCUT - BLOCKCUT_END;   // 15328
 constexpr int HALF = BLOCKLEN / 2;                     // 8192-point complex FFTs
 constexpr int MAX_BLOCKS_PER_READ = 66;
 constexpr int PARK_SLOTS = 2048;                       // demod odd-half parks: one per physical CU (demod.hip)
+constexpr int PARK_EXTRA = 64;                         // spare parks (a CU's park held by a switched-out workgroup)
+constexpr int PARK_SCRATCH = PARK_SLOTS + PARK_EXTRA;  // the shared scratch park (no owner)
+constexpr int PARK_TOTAL = PARK_SCRATCH + 1;
+constexpr int PARK_OWNERS = PARK_SLOTS + PARK_EXTRA;   // owner words
 constexpr int READLEN = 1000000;
 constexpr int MAX_NOUT = READLEN + 1026 + 16;          // end - start + 1 (+ slack)
 constexpr int AUDIO_DIV1 = 16;                         // 40 MHz -> 2.5 MHz (blocklen / 1024)

@@ -179,10 +179,11 @@ __device__ __forceinline__ void st_pair(double* a, double2 z) {
 // The odd-half park's stores (read back by LDS-DMA on the same CU): plain
 // stores ("nt" measured +1.5%, "sc0" even).
 __device__ __forceinline__ void st_park(double2* a, double2 z) { *a = z; }
-// The park's owner words: PARK_SLOTS 64-bit words after the parks (ospill + PARK_SLOTS * M),
-// word u = the tag of the last workgroup that claimed park u (see demod_body).
+// The parks' owner words: PARK_SLOTS + PARK_EXTRA 64-bit words after the parks and the
+// scratch park (ospill + PARK_TOTAL * M); word u = the tag of the workgroup holding park
+// u, 0 when free (see demod_body).
 __device__ __forceinline__ unsigned long long* park_owner(double2* ospill) {
-  return reinterpret_cast<unsigned long long*>(ospill + (int64_t)PARK_SLOTS * M);
+  return reinterpret_cast<unsigned long long*>(ospill + (int64_t)PARK_TOTAL * M);
 }
 __device__ __forceinline__ void store_pair(double* o, int m, double2 z, int copylen) {
   const int p = 2 * m;
@@ -316,7 +317,7 @@ __device__ unsigned long long g_stamps[LDG_STAMP_BLOCKS][32];
 #endif
 
 // grid: n_reads * MAX_BLOCKS_PER_READ workgroups of 1024 threads.
-// ospill: PARK_SLOTS x 8192 double2, one odd-half park per physical CU.
+// ospill: PARK_TOTAL x 8192 double2 parks (one per physical CU, spares, scratch) + owner words.
 #define LDG_DEMOD_PARAMS                                                                                          \
   const int32_t *__restrict__ smap, const ReadDesc *__restrict__ reads, const uint8_t *__restrict__ cap,          \
       int64_t cap_first, int64_t cap_nsamp, int fmt, const double2 *__restrict__ tw,                             \
@@ -371,14 +372,28 @@ __device__ __forceinline__ void demod_body(LDG_DEMOD_PARAMS) {
   // One park per physical CU (one demod workgroup per CU at a time: 128 KiB of
   // LDS), so consecutive workgroups on a CU rewrite the same 128 KiB and it
   // stays cache-resident instead of streaming 1 GB per launch through HBM.
+  //
+  // The park is owned exclusively from its claim to its release: its owner word goes
+  // from 0 to this workgroup's tag (unique per launch and workgroup) by compare-and-swap,
+  // and back to 0 once the reload has completed.  A CU's park is free whenever a
+  // workgroup starts there, unless compute-wave save/restore (a shared or oversubscribed
+  // GPU) switched out the workgroup that holds it: the claimant then takes one of
+  // PARK_EXTRA spare parks, and with all of those held too it runs on the scratch park
+  // (shared, unowned) and flags its read FS_MIGRATED (the host decodes it again).  No
+  // workgroup can store into a park another one holds, so a read not flagged is exact.
+  __shared__ int s_park;
   const int my_cu = cu_slot();
-  double2* park = ospill + (int64_t)my_cu * M;
-  // Claim the park before any store to it: its owner word takes this workgroup's tag
-  // (unique per launch and workgroup), made visible before the park stores (the
-  // fence below, ahead of the barrier that precedes them).  See the check at the reload.
-  unsigned long long* owner = park_owner(ospill) + my_cu;
+  unsigned long long* const owners = park_owner(ospill);
   const unsigned long long my_tag = (park_epoch << 32) | (unsigned long long)blockIdx.x;
-  if (tid == 0) __hip_atomic_store(owner, my_tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  int my_park = -1;                                 // (thread 0) the park this workgroup holds
+  if (tid == 0) {
+    if (atomicCAS(owners + my_cu, 0ull, my_tag) == 0ull) my_park = my_cu;
+    for (int e = 0; e < PARK_EXTRA && my_park < 0; e++) {
+      const int u = PARK_SLOTS + ((my_cu + e) & (PARK_EXTRA - 1));
+      if (atomicCAS(owners + u, 0ull, my_tag) == 0ull) my_park = u;
+    }
+    s_park = my_park;                               // read after the first transform's barriers
+  }
   constexpr double TAU = 6.283185307179586;
 
   // ---- 1. raw samples -> z[m] = x[2m] + i x[2m+1]; forward FFT ---------------
@@ -408,18 +423,12 @@ __device__ __forceinline__ void demod_body(LDG_DEMOD_PARAMS) {
       X_[m] = make_double2(load_sample(cap, fmt, rel0 + 2 * m), load_sample(cap, fmt, rel0 + 2 * m + 1));
     }
   }
-  // The claim is visible before any park store: it is an agent-coherent store (the
-  // atomic store above), so its completion -- vmcnt, which wave 0 has all but reached
-  // by consuming its sample loads issued after it -- is its visibility, and the
-  // barriers before the park stores order them after it.  (A release fence here
-  // would also write back the XCD's whole L2 -- buffer_wbl2 -- on every block: with
-  // it the demod ran 4% slower.)  Every workgroup that can reach this CU's park runs
-  // on this XCD, whose L2 serves all their park stores and reloads.
-  if (tid == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   STAMP(1);
   if (!(kProbe & 8)) fft8k_dif<false>(s_x, tw, twl, tid);
   else __syncthreads();
   STAMP(2);
+  const bool park_lost = s_park < 0;
+  double2* const park = ospill + (int64_t)(park_lost ? PARK_SCRATCH : s_park) * M;
 
   // ---- 2. analytic-signal spectra and the audio carrier slices ---------------
   // Y = X * RFVideo*MTF^m; the 16384-point IFFT of Y is done as its even/odd
@@ -481,29 +490,13 @@ __device__ __forceinline__ void demod_body(LDG_DEMOD_PARAMS) {
   // One loop body for both halves: one copy of the inverse FFT in the code (the
   // kernel would outgrow the instruction cache with every transform inlined).
   double the[8], tho[8];
-  unsigned long long owner_seen = my_tag;
 #pragma clang loop unroll(disable)
   for (int h = 0; h < 2; h++) {
     STAMP(4 + 2 * h);
-#ifndef LDG_NO_PARK_CHECK   // (timing probes only)
-    if (h == 1 && tid == 0 && !(kProbe & (16 | 256))) {
-      // The park is private to this CU only while no other demod workgroup stores to it
-      // between this one's stores and its reload (just completed: vmcnt(0) and the barrier
-      // above).  Compute-wave save/restore (a shared or oversubscribed GPU) can break that:
-      // this workgroup switched out, another one parking on the CU, this one resumed.  Every
-      // workgroup claims the park (owner word = its tag) and makes the claim visible before
-      // its first park store; so if any foreign store landed before this reload read it, the
-      // foreign claim landed before that, after this workgroup's own claim, and the owner
-      // word read now (device-coherent, after the reload completed) is no longer this
-      // workgroup's tag.  The check is exact: a mismatch flags the read (FS_MIGRATED) and
-      // the host decodes it again; a match proves the reloaded half is this block's own.
-      // (A foreign claim without data stores before the reload flags a read that was in
-      // fact intact: a redo, never a wrong result.)
-      // (read now, compared at the end of the block: the load's latency stays off the
-      // transforms' barriers)
-      owner_seen = __hip_atomic_load(owner, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-#endif
+    // release the park: every wave's reload completed before the barrier that ended the
+    // even half (vmcnt(0)), so no later store into it can reach this block's data
+    if (h == 1 && tid == 0 && my_park >= 0)
+      __hip_atomic_store(owners + my_park, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     double2 zr[8];
     fft8k_dit<true, true>(s_x, tw, twl, tid, zr);
     if (h == 0) {
@@ -665,7 +658,7 @@ __device__ __forceinline__ void demod_body(LDG_DEMOD_PARAMS) {
   // past the read's video cut nothing reads the video, burst or pilot channel (the
   // field kernels check, FS_VCUT): the block ends after the sync channel
   if (CUT && (int64_t)off >= rd.vcut) {
-    if (tid == 0 && owner_seen != my_tag) status[slot] = FS_MIGRATED;
+    if (tid == 0 && park_lost) status[slot] = FS_MIGRATED;
     if (span && tid == 0) atomicMax(&span[1], (unsigned long long)__builtin_amdgcn_s_memrealtime());
     return;
   }
@@ -724,7 +717,7 @@ __device__ __forceinline__ void demod_body(LDG_DEMOD_PARAMS) {
     }
   }
   STAMP(19);
-  if (tid == 0 && owner_seen != my_tag) status[slot] = FS_MIGRATED;
+  if (tid == 0 && park_lost) status[slot] = FS_MIGRATED;
   if (span && tid == 0) atomicMax(&span[1], (unsigned long long)__builtin_amdgcn_s_memrealtime());
 }
 

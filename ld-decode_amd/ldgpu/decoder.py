@@ -560,8 +560,12 @@ class GPUDecoder:
             full = [(native.READ_FULL if k in self.full_keys else 0) |
                     (native.READ_PROBE if probe and k in self.plan_guessed and k not in self.full_keys else 0)
                     for k in keys]
-        self.ctx.decode_reads_async([k[0] for k in keys], [k[1] for k in keys], slots, full)
+        back = self.ctx.decode_reads_async([k[0] for k in keys], [k[1] for k in keys], slots, full)
+        if back is not None:
+            full = back
         if probe:
+            # only the reads the library actually probed (a probe block outside the
+            # resident capture is skipped, its flag cleared)
             import bisect
             for k, f in zip(keys, full):
                 if f & native.READ_PROBE:

@@ -89,6 +89,14 @@ class Filters(C.Structure):
 _lib = None
 
 
+def lib_source_hash():
+    """The source hash (build.py source_hash) of the loaded libldgpu.so: its build stamp, or
+    None when the library carries none (a variant build loaded through LDGPU_LIB)."""
+    lib = load()
+    stamp = lib._name + '.sha256'
+    return open(stamp).read().strip() if os.path.exists(stamp) else None
+
+
 def load(path=None):
     """Load libldgpu.so and declare its signatures (no device access).
     LDGPU_LIB names another build of the same library (profiling variants)."""
@@ -299,7 +307,8 @@ class Context:
         returns the records of the oldest outstanding one.  full: per read flags, READ_FULL
         (or True) exempts it from the video cut (set_video_cut; reads that came back FS_VCUT),
         READ_PROBE moves a predicted start to the sync peak a probe finds (the record's
-        readsample is the start decoded)."""
+        readsample is the start decoded).  Returns the flags as the library left them
+        (READ_PROBE set exactly for the reads probed), or None."""
         s, m, sl = (np.ascontiguousarray(starts, dtype=np.int64), np.ascontiguousarray(mtfs, dtype=np.float64),
                     np.ascontiguousarray(slots, dtype=np.int32))
         f = None if full is None else np.ascontiguousarray(full, dtype=np.uint8)
@@ -307,6 +316,7 @@ class Context:
                                                      None if f is None else f.ctypes.data),
                     'ldg_decode_reads_async2')
         self._pending.append(s.size)
+        return f
 
     def set_video_cut(self, out_samples):
         """The demod skips the video / burst / pilot channels of blocks whose outputs start at

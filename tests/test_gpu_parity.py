@@ -283,48 +283,6 @@ def test_end_to_end_vs_golden(case, batch):
     print('%s batch=%d: %d/%d frames bit-identical' % (case, batch, exact, len(got)))
 
 
-@pytest.mark.parametrize('case', ['ntsc_cav_u8_mtf_0p3s', 'pal_cav_u8_mtf_0p3s', 'ntsc_cav_lds_0p15s'])
-def test_demod2_end_to_end_vs_golden(case):
-    """The register-resident demod (demod2.hip, LDG_DEMOD2=1: 512-thread workgroups, claimed
-    park slots, layout-ordered filter tables) gives the golden decode too: metadata exact,
-    .tbc +-1 LSB, .pcm bit-exact (NTSC and PAL, the MTF chain, a 10-bit format).  It is
-    the variant library libldgpu_demod2.so (build.py), so the check runs in a child process
-    that loads it."""
-    import subprocess
-    import sys
-    here = os.path.dirname(os.path.abspath(__file__))
-    root = os.path.dirname(here)
-    lib = os.path.join(root, 'ld-decode_amd', 'ldgpu', 'libldgpu_demod2.so')
-    assert os.path.exists(lib), 'build the variant: __graft_entry__.build()'
-    env = dict(os.environ, LDGPU_LIB=lib, LDG_DEMOD2='1',
-               PYTHONPATH=os.pathsep.join([os.path.join(root, 'ld-decode_amd'), root, here]))
-    r = subprocess.run([sys.executable, '-c', 'import test_gpu_parity as t; t.demod2_check(%r)' % case],
-                       cwd=here, env=env, timeout=240, capture_output=True, text=True)
-    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
-
-
-def demod2_check(case):
-    from ldgpu.decoder import GPUDecoder
-    from ldgpu.formats import NAME_TO_FMT
-    data, gold, frames, pcm, meta = oracle_decode(case)
-    c = gold['settings']
-    dec = GPUDecoder(system=c['system'], batch=8)
-    dec.set_capture(data, NAME_TO_FMT[c['fmt']])
-    for m in (0.88, 0.0):          # its rf table layout (ldg_k_rf_table2) against the oracle's filter
-        from oracle.demod import RFDemod
-        F = RFDemod(system=c['system']).Filters
-        ref = F['RFVideo'] * (F['MTF'] ** m) if m else F['RFVideo']
-        assert np.abs(dec.ctx.rf_table(m) - ref).max() / np.abs(ref).max() < 1e-14
-    got = []
-    dec.decode(sink=lambda fr, au, m: got.append((fr.copy(), au.copy(), m)))
-    assert len(got) == len(gold['frames'])
-    for (fr, au, m), f, g in zip(got, frames, gold['frames']):
-        assert m == g['meta']
-        assert np.abs(fr.astype(np.int64) - f.astype(np.int64)).max() <= 1
-        assert hashlib.sha256(au.tobytes()).hexdigest() == g['pcm_sha256']
-    dec.ctx.close()
-
-
 @pytest.mark.parametrize('case', ['ntsc_clv_u8_0p2s', 'pal_clv_u8_0p2s', 'ntsc_cav_u8_mid_0p2s'])
 def test_video_cut_gives_the_same_decode(case, monkeypatch):
     """The demod skips the video / burst / pilot channels of a read's blocks past its video

@@ -35,8 +35,7 @@ def main():
         dec.decode(length=100)
         t1 = time.perf_counter()
         reads, ms = dec.demod_isolated(iters)
-    print(json.dumps({'reads': reads, 'iters': iters, 'ms_per_launch': round(ms, 4), 'decode_s': round(t1 - t0, 2),
-                      'demod2': os.environ.get('LDG_DEMOD2', '0') != '0'}))
+    print(json.dumps({'reads': reads, 'iters': iters, 'ms_per_launch': round(ms, 4), 'decode_s': round(t1 - t0, 2)}))
 
 
 if __name__ == '__main__':

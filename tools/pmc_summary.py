@@ -2,7 +2,8 @@
 demod's issue / LDS / FP64 counters per launch.
 
     python tools/pmc_summary.py gpurun_out/prof/<tag> profiles/<round>_<tag> [gpurun_out/prof/<tag>sq ...]
-    (then copy <prefix>_pmc_traffic.json to profiles/pmc_traffic.json for bench.py)
+    (then copy <prefix>_pmc_traffic.json to profiles/pmc_traffic.json for bench.py; the file
+    carries the library's source hash, and bench.py uses it only for a run of that library)
 
 Traffic per launch = 2 * FETCH_SIZE + WRITE_SIZE (KiB -> bytes), the gfx950
 correction of MI355X_MICROARCH.md (HBM section): FETCH_SIZE counts half of the
@@ -78,6 +79,14 @@ def derived(c):
     return d
 
 
+def lib_stamp():
+    """The source hash libldgpu.so was built from (its build stamp, build.py source_hash), so
+    bench.py attaches these counters only to a run of that same library."""
+    stamp = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), 'ld-decode_amd', 'ldgpu',
+                         'libldgpu.so.sha256')
+    return open(stamp).read().strip() if os.path.exists(stamp) else None
+
+
 def main(src, dst_prefix, *sq_srcs):
     stats = os.path.join(src, 'trace', 'run_kernel_stats.csv')
     if os.path.exists(stats):
@@ -93,7 +102,8 @@ def main(src, dst_prefix, *sq_srcs):
         fetch, write = c['FETCH_SIZE'] * 1024.0, c['WRITE_SIZE'] * 1024.0
         out[short(k)] = 2 * fetch + write
         rows.append((short(k)[:40], fetch, write, 2 * fetch + write))
-    res = {'unit': 'bytes per launch (2*FETCH_SIZE + WRITE_SIZE)', 'source': src, 'kernels': out}
+    res = {'unit': 'bytes per launch (2*FETCH_SIZE + WRITE_SIZE)', 'source': src, 'kernels': out,
+           'lib_source_sha256': lib_stamp()}
     for k, c in cs.items():
         if short(k) in ('demod_iso', 'demod_iso_cut', 'demod') and any(x.startswith('SQ_') for x in c):
             res[short(k) + '_sq'] = {'per_launch': {x: v for x, v in sorted(c.items())}, 'derived': derived(c)}
