@@ -162,6 +162,34 @@ int ldg_set_filters(ldg_ctx* ctx, const ldg_params* p, const ldg_filters* f);
 int ldg_set_capture(ldg_ctx* ctx, const void* data, int64_t nsamples, int fmt, int64_t first_sample,
                     int is_device);
 
+/* ---- streamed capture (replaces RFDecode's per-block loader calls,
+ * lddecode_core.py:373-392 -> lddutils.py:131-229, for a capture of any length) ----
+ * ldg_stream_open makes the file at `path` (format fmt, as ldg_set_capture) the capture,
+ * streamed from storage by a reader thread through pinned staging into a ring of
+ * ring_bytes in HBM (device memory independent of the file's length; rounded down to
+ * the reader's chunk), starting at first_sample's packing group.  Decodes then read it
+ * as a resident capture, with two rules:
+ *   - a launch waits until the samples its reads need have been read (overlapped:
+ *     the reader runs ahead as far as the ring allows);
+ *   - the host releases what it will not read again: ldg_stream_release(below) lets
+ *     the reader overwrite samples below `below` once the launches issued so far have
+ *     finished.  A launch whose reads end past the ring's reach (ldg_stream_window
+ *     out[1]) fails with LDG_ESTATE; reads starting below the released point come back
+ *     LDG_FS_EOF.
+ * ldg_stream_seek restarts the stream at another sample (no decode outstanding).
+ * ldg_set_capture, ldg_synth_capture and ldg_destroy close the stream. */
+int ldg_stream_open(ldg_ctx* ctx, const char* path, int fmt, int64_t ring_bytes, int64_t first_sample);
+int ldg_stream_release(ldg_ctx* ctx, int64_t below_sample);
+int ldg_stream_seek(ldg_ctx* ctx, int64_t first_sample);
+/* out[0..3]: the lowest sample a launch may read, the highest block end it may reach,
+ * the samples read so far, the capture's total samples. */
+int ldg_stream_window(ldg_ctx* ctx, int64_t* out4);
+/* Up to n doubles: bytes read, seconds in read(2), chunks, launches that waited for data,
+ * seconds they waited, seconds the reader waited for ring space, seeks, ring bytes, chunk
+ * bytes.  Returns the count written. */
+int ldg_stream_stats(ldg_ctx* ctx, double* out, int n);
+int ldg_stream_close(ldg_ctx* ctx);
+
 /* Demodulate and analyse n field reads: read i starts at read_starts[i] (the
  * `start` argument of RFDecode.demod, readlen 1,000,000) with MTF level
  * mtf[i] and is stored in device slot slots[i] (0 <= slot < max_reads,

@@ -318,9 +318,13 @@ __device__ unsigned long long g_stamps[LDG_STAMP_BLOCKS][32];
 
 // grid: n_reads * MAX_BLOCKS_PER_READ workgroups of 1024 threads.
 // ospill: PARK_TOTAL x 8192 double2 parks (one per physical CU, spares, scratch) + owner words.
+// cap: the resident capture samples [cap_first, cap_first + cap_nsamp); ring = 0: cap holds
+// them from its start; ring > 0 (a streamed capture, ldg_stream_open): cap is a ring of
+// `ring` bytes (a multiple of every format's packing group) where the capture's byte b lives
+// at b mod ring, followed by a mirror of its first bytes, so one block is contiguous.
 #define LDG_DEMOD_PARAMS                                                                                          \
   const int32_t *__restrict__ smap, const ReadDesc *__restrict__ reads, const uint8_t *__restrict__ cap,          \
-      int64_t cap_first, int64_t cap_nsamp, int fmt, const double2 *__restrict__ tw,                             \
+      int64_t cap_first, int64_t cap_nsamp, int64_t ring, int fmt, const double2 *__restrict__ tw,               \
       const double2 *__restrict__ twk, const double2 *__restrict__ rf_filt, const double2 *__restrict__ g_video,  \
       const double2 *__restrict__ g_05, const double *__restrict__ iir, const double2 *__restrict__ a_lfilt,      \
       const double2 *__restrict__ a_rfilt, SysConst C, double *__restrict__ video, int64_t vread_stride,          \
@@ -330,7 +334,7 @@ __device__ unsigned long long g_stamps[LDG_STAMP_BLOCKS][32];
       double2 *__restrict__ aslice, double *__restrict__ sst, uint32_t *__restrict__ sbits,                      \
       double4 *__restrict__ bst, unsigned long long *__restrict__ span
 #define LDG_DEMOD_ARGS                                                                                            \
-  smap, reads, cap, cap_first, cap_nsamp, fmt, tw, twk, rf_filt, g_video, g_05, iir, a_lfilt, a_rfilt, C, video, \
+  smap, reads, cap, cap_first, cap_nsamp, ring, fmt, tw, twk, rf_filt, g_video, g_05, iir, a_lfilt, a_rfilt, C, video, \
       vread_stride, vchan_stride, audio1, aread_stride, achan_stride, status, ospill, park_epoch, stiles, aslice,  \
       sst, sbits,                                                                                                 \
       bst, span
@@ -360,10 +364,18 @@ __device__ __forceinline__ void demod_body(LDG_DEMOD_PARAMS) {
   const int64_t i0 = rd.s0 + (int64_t)b * BLOCKSTEP;
   const int off = b * BLOCKSTEP;
   const int copylen = (off + (BLOCKLEN - BLOCKCUT) > rd.n_out) ? rd.n_out - off : BLOCKSTEP;
-  const int64_t rel0 = i0 - cap_first;
+  int64_t rel0 = i0 - cap_first;
   if (rel0 < 0 || rel0 + BLOCKLEN > cap_nsamp) {
     if (tid == 0) status[slot] = FS_EOF;
     return;
+  }
+  if (ring) {
+    // streamed capture: the block's first packing group at its ring position, the block
+    // read from there (contiguous through the ring's mirrored head)
+    const int spg = fmt == 2 ? 3 : fmt == 3 ? 4 : 1, bpg = fmt == 1 ? 2 : fmt == 2 ? 4 : fmt == 3 ? 5 : 1;
+    const int64_t g = i0 / spg;
+    cap += (g * bpg) % ring;
+    rel0 = i0 - g * spg;
   }
   double* vout = video + (int64_t)slot * vread_stride + off - BLOCKCUT;   // index by block position p
   const double2* F = rf_filt + (int64_t)rd.filt_slot * BLOCKLEN;

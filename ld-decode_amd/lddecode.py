@@ -16,7 +16,10 @@ comb-ntsc -d 3 -F's).  The comb alone, on a .tbc stream: comb_ntsc.py.
 import argparse
 import json
 import os
+import queue
 import sys
+import threading
+import time
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, HERE)
@@ -25,6 +28,56 @@ import numpy as np  # noqa: E402
 
 from ldgpu.decoder import GPUDecoder  # noqa: E402
 from ldgpu.formats import fmt_from_path, read_samples, samples_in_bytes  # noqa: E402
+
+
+class Writer:
+    """The decode's outputs written on a thread of their own, in order: the reference's
+    loop writes each frame and prints its lines between decodes (lddecode.py:88-98);
+    here the decode thread queues those writes and goes on decoding.  The frames it
+    queues are views of the decoder's pinned output rings: drain() (the decoder's
+    before_ring_reuse hook) returns once every queued write is done, before a ring is
+    filled again."""
+
+    def __init__(self):
+        self.q = queue.Queue()
+        self.err = None
+        self.busy_s = self.drain_s = 0.0
+        self.t = threading.Thread(target=self._run, name='ldg-writer', daemon=True)
+        self.t.start()
+
+    def _run(self):
+        while True:
+            fn = self.q.get()
+            try:
+                if fn is None:
+                    return
+                if self.err is None:
+                    t0 = time.perf_counter()
+                    fn()
+                    self.busy_s += time.perf_counter() - t0
+            except BaseException as e:     # reported on the decode thread
+                self.err = e
+            finally:
+                self.q.task_done()
+
+    def put(self, fn):
+        if self.err is not None:
+            raise self.err
+        self.q.put(fn)
+
+    def drain(self):
+        t0 = time.perf_counter()
+        self.q.join()
+        self.drain_s += time.perf_counter() - t0
+        if self.err is not None:
+            raise self.err
+
+    def close(self):
+        if self.t.is_alive():
+            self.q.put(None)
+            self.t.join()
+        if self.err is not None:
+            raise self.err
 
 
 def parse(argv=None):
@@ -57,6 +110,11 @@ def parse(argv=None):
                    help="comb-ntsc options for --comb (NTSC), e.g. '-I 0 -N 1 -v' (comb_ntsc.py's -I -b -n -N "
                         "-B -a -L -Q -v -l -W)")
     p.add_argument('--no-json', action='store_true', help='do not write <outfile>.json')
+    p.add_argument('--stats-json', default=None,
+                   help='one process: write a timing breakdown of the run (read, decode, write) to this file')
+    p.add_argument('--window-mb', type=int, default=2048,
+                   help='one process: the capture streams from the file through a ring of this many MiB of HBM '
+                        '(device memory independent of the capture length); 0: upload the whole capture')
     p.add_argument('--epoch-frames', type=int, default=0,
                    help='decode in epochs of N frames, each a complete (sharded) decode whose outputs are final '
                         'before the next starts; with --manifest a crashed run resumes at the last finished epoch')
@@ -123,7 +181,10 @@ def main(argv=None):
 
     fmt = fmt_from_path(filename)
     raw = np.memmap(filename, dtype=np.uint8, mode='r')
-    if world == 1 or args.seek >= 0 or args.cut:
+    if world == 1 and args.window_mb > 0:
+        # streamed from storage through an HBM ring, the read overlapped with the decode
+        dec.open_stream(filename, fmt, args.window_mb << 20, first_sample=firstframe * dec.rf.samples_per_frame)
+    elif world == 1 or args.seek >= 0 or args.cut:
         dec.set_capture(raw, fmt)
     else:
         dec.cap_bytes, dec.cap_nsamples, dec.fmt = infile_size, samples_in_bytes(fmt, infile_size), fmt
@@ -157,18 +218,34 @@ def main(argv=None):
     pcm = open(outname + '.pcm', 'wb')
     rgb = open(outname + '.rgb', 'wb') if args.comb else None
     meta_all = []
+    w = Writer()
 
     def sink(frame, audio, meta):
-        print('frame ', meta['vbi']['framenr'])
-        tbc.write(frame.tobytes())
-        pcm.write(audio.tobytes())
-        meta_all.append(meta)
+        def write():
+            print('frame ', meta['vbi']['framenr'])
+            tbc.write(np.ascontiguousarray(frame))
+            pcm.write(np.ascontiguousarray(audio))
+            meta_all.append(meta)
+        w.put(write)
 
-    dec.frame_log = lambda lines: print('\n'.join(lines))    # the reference's per-field lines
-    n = dec.decode(start_frame=firstframe, length=num_frames, sink=sink, comb=args.comb,
-                   comb_sink=(lambda r: rgb.write(r.tobytes())) if rgb else None,
-                   start_sample=nextsample,
-                   comb3d=(args.comb_3d_core, args.comb_3d_range) if args.comb_3d else None)
+    def comb_sink(r):
+        w.put(lambda: rgb.write(np.ascontiguousarray(r)))
+
+    def frame_log(lines):
+        w.put(lambda: print('\n'.join(lines)))   # the reference's per-field lines
+
+    dec.frame_log = frame_log
+    dec.before_ring_reuse = w.drain
+    t0 = time.perf_counter()
+    try:
+        n = dec.decode(start_frame=firstframe, length=num_frames, sink=sink, comb=args.comb,
+                       comb_sink=comb_sink if rgb else None, start_sample=nextsample,
+                       comb3d=(args.comb_3d_core, args.comb_3d_range) if args.comb_3d else None)
+        t_dec = time.perf_counter() - t0
+        w.close()
+    finally:
+        dec.before_ring_reuse = None
+        w.close()
     if req_frames is not None and n < req_frames:
         print('Warning: end of file reached before requested number of frames were decoded')
     tbc.close()
@@ -178,7 +255,32 @@ def main(argv=None):
     if not args.no_json:
         with open(outname + '.json', 'w') as fh:
             json.dump(meta_all, fh)
+    t_all = time.perf_counter() - t0
+    if args.stats_json:
+        write_stats(args.stats_json, dec, n, meta_all, t_dec, t_all, w)
     return 0
+
+
+def write_stats(path, dec, n, metas, t_dec, t_all, w):
+    """The run's timing breakdown (one process): where the wall time went between
+    reading the file, the decode, and writing the outputs."""
+    first = metas[0]['fields'][0]['readsample'] if metas else 0
+    consumed = (metas[-1]['nextsample'] - first) if metas else 0
+    st = dec.stats
+    out = {'frames': n, 'rf_samples_consumed': consumed, 'decode_wall_s': round(t_dec, 4),
+           'total_wall_s': round(t_all, 4),
+           'rf_msamples_per_s': round(consumed / t_all / 1e6, 3) if t_all else None,
+           'fields_per_s': round(2 * n / t_all, 1) if t_all else None,
+           'decode_thread_s': {k: round(st.get(k, 0.0), 4) for k in ('plan_s', 'gpu_s', 'replay_s', 'flush_s',
+                                                                       'wait_s')},
+           'writer': {'busy_s': round(w.busy_s, 4), 'decode_waited_s': round(w.drain_s, 4)},
+           'reads_decoded': st.get('reads'), 'reads_used': st.get('reads_used'),
+           'stream_seeks': st.get('stream_seeks', 0)}
+    if dec.stream:
+        s = dec.ctx.stream_stats()
+        out['stream'] = dict(s, read_gbs=round(s['bytes_read'] / max(s['read_s'], 1e-9) / 1e9, 3))
+    with open(path, 'w') as fh:
+        json.dump(out, fh, indent=1)
 
 
 def load_window(dec, raw, fmt, rank, world, start, rccl, start_frame=0, length=None):

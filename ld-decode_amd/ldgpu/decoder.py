@@ -30,6 +30,10 @@ from .rfparams import RFTables
 
 READLEN = 1000000
 BLOCKLEN, BLOCKCUT, BLOCKSTEP = 16384, 1024, 15328
+# a streamed capture keeps this many samples below the replay's position: a read's first
+# block (start - 1024) and its start probe's block (start - 7664 - 1024, moved by up to
+# 0.3 lines) begin there at most
+STREAM_MARGIN = 32768
 
 
 class Miss(Exception):
@@ -217,6 +221,7 @@ class GPUDecoder:
         self.cap_bytes = None
         self.cap_nsamples = None
         self.window = None          # (first, end) samples resident when a capture window is set
+        self.stream = False         # the capture streams from its file (open_stream)
         self.cache = {}            # (start, mtf) -> (slot, info)
         self.hints = {}            # start -> absolute next start (start + nextfieldoffset)
         self._hint_keys = []       # sorted starts with hints
@@ -285,6 +290,7 @@ class GPUDecoder:
         self.frame_log = None              # callback(lines): the reference's stdout lines of each frame
         self._obufs = None                 # pinned host rings for the asynchronous output path
         self._oring = 0
+        self.before_ring_reuse = None      # callback: the sink's use of the frames handed over is done
 
     # ---- capture ---------------------------------------------------------------
     def set_capture(self, data, fmt, device_ptr=None, nsamples=None, first_sample=0, total_bytes=None):
@@ -295,6 +301,7 @@ class GPUDecoder:
         of total_bytes bytes; the frame accounting (EOF guard, frame count) uses the
         whole capture, and a read that needs samples outside the window raises
         WindowMiss instead of ending the decode."""
+        self.stream = False
         if device_ptr is None:
             buf = np.frombuffer(data, dtype=np.uint8) if not isinstance(data, np.ndarray) else data.view(np.uint8)
             nbytes = buf.size
@@ -312,8 +319,43 @@ class GPUDecoder:
             self.cap_nsamples = samples_in_bytes(fmt, self.cap_bytes)
         self._reset_cache()
 
+    def open_stream(self, path, fmt, ring_bytes, first_sample=0):
+        """Stream the capture from its file (ldg_stream_open): the reference's loader reads
+        each block from the file as the demod needs it (lddecode_core.py:373-392,
+        lddutils.py:131-229), so device memory stays at ring_bytes whatever the capture's
+        length; a reader thread keeps the ring filled ahead of the decode, and the decode
+        releases what its replay has passed (STREAM_MARGIN below its position)."""
+        self.ctx.stream_open(path, fmt, ring_bytes, first_sample)
+        self.window = None
+        self.stream = True
+        self.fmt, self.cap_bytes = fmt, os.path.getsize(path)
+        self.cap_nsamples = samples_in_bytes(fmt, self.cap_bytes)
+        self._reset_cache()
+
+    def _stream_fit(self, keys):
+        """The leading keys a launch can decode from the stream's ring now: none below its
+        lowest readable sample, none ending past its reach.  With nothing in flight and no
+        key fitting, the stream restarts at the first key (a jump of the replay, a seek)."""
+        def span(k):
+            s0, _, last = read_geometry(k[0])
+            return s0, min(last + BLOCKLEN, self.cap_nsamples)
+        for attempt in range(2):
+            lo, reach, _, _ = self.ctx.stream_window()
+            n = 0
+            for k in keys:
+                a, b = span(k)
+                if a < lo or b > reach:
+                    break
+                n += 1
+            if n or self.pending or attempt or not keys:
+                return keys[:n]
+            self.stats['stream_seeks'] = self.stats.get('stream_seeks', 0) + 1
+            self.ctx.stream_seek(max(0, span(keys[0])[0] - STREAM_MARGIN))
+        return keys[:0]
+
     def use_resident_capture(self, fmt, nsamples):
         """The capture already lives in this context's HBM (e.g. Context.synth)."""
+        self.stream = False
         self.window = None
         self.fmt, self.cap_nsamples = fmt, nsamples
         self.cap_bytes = bytes_for_samples(fmt, nsamples)
@@ -534,6 +576,12 @@ class GPUDecoder:
         entries not in `protect` (the reads the replay is about to consume) as
         needed; _launch_wait() adds the records of the oldest launch to the cache.
         Slots of launches still in flight are never reused."""
+        if self.stream:
+            keys = self._stream_fit(keys)
+            if not keys:
+                if self.pending:
+                    return False            # the ring moves on once the replay releases
+                raise RuntimeError('stream: a read does not fit the ring (ring too small for one read)')
         used = {v[0] for v in self.cache.values()}
         for _, sl in self.pending:
             used.update(sl)
@@ -688,6 +736,9 @@ class GPUDecoder:
         slot, info = hit
         if info.status == native.FS_CRASH:
             raise ReferenceCrash('reference would raise at read %d' % readsample)
+        if info.status == native.FS_EOF and self.stream:
+            if read_geometry(key[0])[2] + BLOCKLEN <= self.cap_nsamples:
+                raise RuntimeError('stream: read %d came back FS_EOF inside the capture' % key[0])
         if info.status == native.FS_EOF and self.window is not None:
             s0, _, last = read_geometry(key[0])
             if s0 < self.window[0] or last + BLOCKLEN > self.window[1]:
@@ -914,6 +965,8 @@ class GPUDecoder:
                     self._out_pending = None
                     self._staged, self._staged_slots = None, set()
                     self.ctx.sync()
+                    if self.before_ring_reuse is not None:
+                        self.before_ring_reuse()   # the sink's writes from the rings are done
                     for ring in self._obufs or ():
                         for b in ring:
                             b.release_retired()
@@ -1017,6 +1070,9 @@ class GPUDecoder:
                 frames.append(fr)
                 hist = (hist + [x.readsample for x in self.field_log if x.valid])[-self.hist_len:]
             self.stats['replay_s'] += time.perf_counter() - t0
+            if self.stream:
+                # the replay never reads before its checkpoint again: the reader may refill that
+                self.ctx.stream_release(nextsample - STREAM_MARGIN)
             if self.stats['batches'] % 32 == 0:
                 gc.collect(1)
             if self.stats['batches'] % 512 == 0:
@@ -1076,6 +1132,8 @@ class GPUDecoder:
             tb, rb = self._obufs[self._oring]
             self._oring ^= 1
             n = len(frames)
+            if self.before_ring_reuse is not None:
+                self.before_ring_reuse()           # (a sink that writes its frames later, lddecode.py Writer)
             pics = tb.view(n * H * W).reshape(n, H * W)
             rgb = rb.view(n * rh * rw * 3).reshape(n, rh, rw, 3) if self.comb else None
             self.ctx.output_async(tops, bots, pics, rgb)

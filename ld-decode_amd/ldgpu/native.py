@@ -27,7 +27,11 @@ EXPORTS = ['ldg_create', 'ldg_destroy', 'ldg_last_error', 'ldg_set_filters', 'ld
            'ldg_archive_fields', 'ldg_archive_audio', 'ldg_decode_reads_async', 'ldg_decode_reads_async2',
            'ldg_set_video_cut', 'ldg_decode_reads_wait',
            'ldg_field_audio_async', 'ldg_field_audio_collect', 'ldg_comb_ntsc3d', 'ldg_cx_create', 'ldg_cx_destroy', 'ldg_cx_process', 'ldg_comb_pal', 'ldg_comb_set_state', 'ldg_profile_spans', 'ldg_profile_spans_union', 'ldg_profile_span_table',
-           'ldg_audio_offsets', 'ldg_comb_async', 'ldg_debug_rf_table']
+           'ldg_audio_offsets', 'ldg_comb_async', 'ldg_debug_rf_table',
+           'ldg_stream_open', 'ldg_stream_release', 'ldg_stream_seek', 'ldg_stream_window', 'ldg_stream_stats',
+           'ldg_stream_close']
+STREAM_STATS = ('bytes_read', 'read_s', 'chunks', 'launch_waits', 'launch_wait_s', 'space_wait_s', 'seeks',
+                'ring_bytes', 'chunk_bytes')     # ldg_stream_stats, in order
 
 
 class FieldInfo(C.Structure):
@@ -159,6 +163,12 @@ def load(path=None):
     lib.ldg_cx_destroy.argtypes = [vp]
     lib.ldg_cx_process.argtypes = [vp, C.c_int64, vp, vp]
     lib.ldg_audio_offsets.argtypes = [C.c_double, C.c_int64, vp, C.c_double, vp]
+    lib.ldg_stream_open.argtypes = [vp, C.c_char_p, C.c_int, C.c_int64, C.c_int64]
+    lib.ldg_stream_release.argtypes = [vp, C.c_int64]
+    lib.ldg_stream_seek.argtypes = [vp, C.c_int64]
+    lib.ldg_stream_window.argtypes = [vp, vp]
+    lib.ldg_stream_stats.argtypes = [vp, vp, C.c_int]
+    lib.ldg_stream_close.argtypes = [vp]
     lib.ldg_version.restype = C.c_char_p
     lib.ldg_device_count.restype = C.c_int
     _lib = lib
@@ -282,6 +292,36 @@ class Context:
             buf = np.ascontiguousarray(buf)
             rc = self.lib.ldg_set_capture(self.h, buf.ctypes.data_as(C.c_void_p), nsamples, fmt, first_sample, 0)
         self._check(rc, 'ldg_set_capture')
+
+    # ---- streamed capture (ldg_stream_*) -------------------------------------------
+    def stream_open(self, path, fmt, ring_bytes, first_sample=0):
+        """Stream the capture file at `path` through an HBM ring of ring_bytes (see
+        include/ldgpu.h); replaces any resident capture."""
+        self._check(self.lib.ldg_stream_open(self.h, os.fsencode(path), int(fmt), int(ring_bytes), int(first_sample)),
+                    'ldg_stream_open')
+
+    def stream_release(self, below_sample):
+        self._check(self.lib.ldg_stream_release(self.h, int(below_sample)), 'ldg_stream_release')
+
+    def stream_seek(self, first_sample):
+        self._check(self.lib.ldg_stream_seek(self.h, int(first_sample)), 'ldg_stream_seek')
+
+    def stream_window(self):
+        """(lowest readable sample, highest block end a launch may reach, samples read so far,
+        total samples)"""
+        out = np.zeros(4, dtype=np.int64)
+        self._check(self.lib.ldg_stream_window(self.h, out.ctypes.data), 'ldg_stream_window')
+        return tuple(int(x) for x in out)
+
+    def stream_stats(self):
+        out = np.zeros(len(STREAM_STATS), dtype=np.float64)
+        n = self.lib.ldg_stream_stats(self.h, out.ctypes.data, out.size)
+        if n < 0:
+            self._check(n, 'ldg_stream_stats')
+        return dict(zip(STREAM_STATS[:n], (float(x) for x in out[:n])))
+
+    def stream_close(self):
+        self._check(self.lib.ldg_stream_close(self.h), 'ldg_stream_close')
 
     def decode_reads(self, starts, mtfs, slots=None):
         n = len(starts)
