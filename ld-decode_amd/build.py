@@ -78,5 +78,26 @@ def build(force=False, verbose=True):
     return OUT
 
 
+ASAN = os.path.join(HERE, 'ldgpu', 'libldgpu_asan.so')
+# the host side under AddressSanitizer + UndefinedBehaviorSanitizer (device code as usual:
+# GPU sanitizers are not used on this pool); for tests/san's CPU drivers only, never loaded
+# by the decode path
+ASAN_FLAGS = ['-Xarch_host', '-fsanitize=address', '-Xarch_host', '-fsanitize=undefined',
+              '-Xarch_host', '-fno-sanitize-recover=all', '-Xarch_host', '-fno-omit-frame-pointer',
+              '-Xarch_host', '-g']
+
+
+def build_asan(verbose=True):
+    cmd = [HIPCC] + FLAGS + ASAN_FLAGS + [os.path.join(CSRC, 'ldgpu.hip'), '-o', ASAN + '.tmp']
+    if verbose:
+        print('compiling libldgpu_asan.so: ' + ' '.join(cmd), flush=True)
+    subprocess.run(cmd, check=True, cwd=CSRC)
+    os.replace(ASAN + '.tmp', ASAN)
+    return ASAN
+
+
 if __name__ == '__main__':
-    build(force='--force' in sys.argv)
+    if '--asan' in sys.argv:
+        build_asan()
+    else:
+        build(force='--force' in sys.argv)

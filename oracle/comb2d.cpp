@@ -211,7 +211,9 @@ struct Comb {
         }
         for (int j = 5; j <= 831; j++) {       // _k[h - 8] = lp_3d.feed(__k(h)), h = 13..839
           double y0 = 0;
-          for (int t = 0; t < 17; t++) y0 += (LP3D_B[t] / 1.0) * x[j + 8 - t];
+          // the filter's history before its first feed is zero: taps reaching before x[0]
+          // (j + 8 - t < 0 for j = 5..7) add 0 (an out-of-bounds read before tests/san's ASan run)
+          for (int t = 0; t < 17; t++) y0 += (LP3D_B[t] / 1.0) * (j + 8 - t >= 0 ? x[j + 8 - t] : 0.0);
           kk[j] = y0;
         }
         for (int h = 4; h < 840; h++) {
