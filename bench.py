@@ -1,7 +1,7 @@
 """Benchmark: RF Msamples/s and fields/s of the MI355X decode path (BASELINE.json metric).
 
     python bench.py [--gpus N --steps K --warmup W]
-    (N > 1: torch.distributed.run, one rank per GPU, weak scaling)
+    (N > 1: torch.distributed.run, one rank per GPU: one capture field-sharded, strong scaling)
 
 N = 1 (default; BASELINE.json configs[1]): 60 s of synthetic NTSC CAV RF,
 40 MSPS, 8-bit, synthesised on the GPU straight into HBM (same signal model as
@@ -30,11 +30,6 @@ sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, 'ld-decode_amd'))
 
 import numpy as np  # noqa: E402
-
-# each of the decode context's streams gets a hardware queue (ldgpu/__init__.py);
-# set before torch (N > 1) initialises the HIP runtime
-if int(os.environ.get('GPU_MAX_HW_QUEUES', '0') or 0) < 12:
-    os.environ['GPU_MAX_HW_QUEUES'] = '12'
 
 NTSC_TBC_BYTES_PER_SAMPLE = 955500 / 1334667
 NTSC_PCM_BYTES_PER_SAMPLE = 0.0048

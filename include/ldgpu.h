@@ -441,6 +441,8 @@ int ldg_cx_process(ldg_cx* cx, int64_t n, const uint16_t* in, uint16_t* out);
 /* Library / device identification. */
 const char* ldg_version(void);
 int ldg_device_count(void);
+/* Free and total device memory of `device` (hipMemGetInfo): what a context holds. */
+int ldg_device_memory(int device, int64_t* free_bytes, int64_t* total_bytes);
 
 #ifdef __cplusplus
 }

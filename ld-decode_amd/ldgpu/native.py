@@ -29,7 +29,7 @@ EXPORTS = ['ldg_create', 'ldg_destroy', 'ldg_last_error', 'ldg_set_filters', 'ld
            'ldg_field_audio_async', 'ldg_field_audio_collect', 'ldg_comb_ntsc3d', 'ldg_cx_create', 'ldg_cx_destroy', 'ldg_cx_process', 'ldg_comb_pal', 'ldg_comb_set_state', 'ldg_profile_spans', 'ldg_profile_spans_union', 'ldg_profile_span_table',
            'ldg_audio_offsets', 'ldg_comb_async', 'ldg_debug_rf_table',
            'ldg_stream_open', 'ldg_stream_release', 'ldg_stream_seek', 'ldg_stream_window', 'ldg_stream_stats',
-           'ldg_stream_close']
+           'ldg_stream_close', 'ldg_device_memory']
 STREAM_STATS = ('bytes_read', 'read_s', 'chunks', 'launch_waits', 'launch_wait_s', 'space_wait_s', 'seeks',
                 'ring_bytes', 'chunk_bytes')     # ldg_stream_stats, in order
 
@@ -169,10 +169,20 @@ def load(path=None):
     lib.ldg_stream_window.argtypes = [vp, vp]
     lib.ldg_stream_stats.argtypes = [vp, vp, C.c_int]
     lib.ldg_stream_close.argtypes = [vp]
+    lib.ldg_device_memory.argtypes = [C.c_int, C.POINTER(C.c_int64), C.POINTER(C.c_int64)]
     lib.ldg_version.restype = C.c_char_p
     lib.ldg_device_count.restype = C.c_int
     _lib = lib
     return lib
+
+
+def device_memory(device=0):
+    """(free, total) bytes of device memory (ldg_device_memory)."""
+    f, t = C.c_int64(), C.c_int64()
+    rc = load().ldg_device_memory(int(device), C.byref(f), C.byref(t))
+    if rc != LDG_OK:
+        raise LDGError('ldg_device_memory failed (%d)' % rc)
+    return f.value, t.value
 
 
 def _ptr(a, t=C.c_double):

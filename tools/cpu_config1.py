@@ -19,6 +19,14 @@ from threadpoolctl import threadpool_limits  # noqa: E402
 
 
 def main(out, seconds=10.0):
+    import threading
+    done = threading.Event()
+    t_start = time.perf_counter()
+
+    def beat():                    # a heartbeat on stderr (long CPU phases print nothing)
+        while not done.wait(30.0):
+            print('[cpu_config1] %.0f s' % (time.perf_counter() - t_start), file=sys.stderr, flush=True)
+    threading.Thread(target=beat, daemon=True).start()
     from ldgpu.synth import make_capture
     from oracle.capture import FMT_U8
     from oracle.framer import decode_capture
@@ -39,6 +47,7 @@ def main(out, seconds=10.0):
            'x_realtime': consumed / dt / 40e6, 'synth_s': round(synth_s, 1),
            'tbc_bytes': len(tbc), 'tbc_sha256': hashlib.sha256(tbc).hexdigest(),
            'framenrs': [m['vbi']['framenr'] for m in meta][:5] + ['...']}
+    done.set()
     with open(out, 'w') as fh:
         json.dump(rec, fh, indent=1)
     print(json.dumps(rec))
