@@ -31,6 +31,11 @@ sys.path.insert(0, os.path.join(ROOT, 'ld-decode_amd'))
 
 import numpy as np  # noqa: E402
 
+# each of the decode context's streams gets a hardware queue (ldgpu/__init__.py);
+# set before torch (N > 1) initialises the HIP runtime
+if int(os.environ.get('GPU_MAX_HW_QUEUES', '0') or 0) < 12:
+    os.environ['GPU_MAX_HW_QUEUES'] = '12'
+
 NTSC_TBC_BYTES_PER_SAMPLE = 955500 / 1334667
 NTSC_PCM_BYTES_PER_SAMPLE = 0.0048
 NTSC_COMB_BYTES_PER_SAMPLE = (955500 + 2142720) / 1334667   # .tbc in + rgb48 out per frame
