@@ -777,8 +777,8 @@ extern "C" __global__ __launch_bounds__(64) void ldg_k_hsync_lines(
 
   __shared__ double s_tmp[20];
   const int lane = threadIdx.x;
-  const int slot = smap[blockIdx.x / MAX_LINES];
-  const int i = blockIdx.x % MAX_LINES;
+  const int slot = smap[blockIdx.y];
+  const int i = blockIdx.x;
   FieldRec* R = recs + slot;
   const double* L1 = lines + (int64_t)slot * LINES_STRIDE + LL1 * MAX_LINES;
   double* L2 = lines + (int64_t)slot * LINES_STRIDE + LL2 * MAX_LINES;

@@ -290,7 +290,7 @@ __device__ inline int calczc_s(const double* d, int len, int s, double target, i
 // Burst pass, per (read, line): resample demod_burst over [li[l], li[l+1]] to
 // 4fsc pixels 20..59 (lineoffset 0, wow-scaled), then the per-line part of
 // refine_linelocs_burst (lddecode_core.py:1069-1110).
-// grid: n_reads * LINE_GROUPS workgroups of 64 threads; lane = line.
+// grid: (lines per read, n_reads) workgroups of 64 threads, one line each.
 extern "C" __global__ __launch_bounds__(64) void ldg_k_burst_lines(
     const int32_t* __restrict__ smap, const double* __restrict__ video, int64_t vread_stride, int64_t vchan_stride, SysConst C,
     FieldRec* __restrict__ recs, double* __restrict__ lines, float* __restrict__ blevel, int pass,
@@ -301,8 +301,8 @@ extern "C" __global__ __launch_bounds__(64) void ldg_k_burst_lines(
   __shared__ SplineLDS<64, 384> S;
   __shared__ double s_ba[40], s_t[40], s_g[2][40];
   const int lane = threadIdx.x;
-  const int slot = smap[blockIdx.x / MAX_LINES];
-  const int l = blockIdx.x % MAX_LINES;
+  const int slot = smap[blockIdx.y];
+  const int l = blockIdx.x;
   FieldRec* R = recs + slot;
   double* LN = lines + (int64_t)slot * LINES_STRIDE;
   const double* li = LN + (pass == 0 ? LL2 : LL3) * MAX_LINES;
@@ -510,7 +510,7 @@ extern "C" __global__ __launch_bounds__(64) void ldg_k_burst_field(const int32_t
 // evaluation's two knots per output straight from the channel) and only the
 // second derivatives in LDS.  ~25 KiB of LDS per workgroup, so a final-pass
 // workgroup fits beside a demod workgroup (128 KiB) on one CU.
-// grid: n_reads * MAX_LINES workgroups of FINAL_NT threads, one line each.
+// grid: (rows per read, n_reads) workgroups of FINAL_NT threads, one line each.
 constexpr int FINAL_NT = 256;
 constexpr int FINAL_CHMAX = ((SPL_MAXN + FINAL_NT - 1) / FINAL_NT) | 1;   // rows per thread, upper bound
 struct FinalLDS {
@@ -564,8 +564,8 @@ __device__ __forceinline__ void final_lines_impl(
   } U;
   FinalLDS& S = U.S;
   const int tid = threadIdx.x;
-  const int slot = smap[blockIdx.x / MAX_LINES];
-  const int row = blockIdx.x % MAX_LINES;
+  const int slot = smap[blockIdx.y];
+  const int row = blockIdx.x;
   FieldRec* R = recs + slot;
   const int loff = (C.system == 1) ? 3 : 1;
   const int l = row + loff;
@@ -901,8 +901,8 @@ extern "C" __global__ __launch_bounds__(64) void ldg_k_pilot_lines(const int32_t
   __shared__ double s_off[PILOT_MAX];
   __shared__ double s_srt[PILOT_MAX];
   const int lane = threadIdx.x;
-  const int slot = smap[blockIdx.x / MAX_LINES];
-  const int l = blockIdx.x % MAX_LINES;
+  const int slot = smap[blockIdx.y];
+  const int l = blockIdx.x;
   FieldRec* R = recs + slot;
   if (R->status != FS_PENDING) return;
   const int nl = R->nlines;
