@@ -155,8 +155,9 @@ def main(argv=None):
             torch.cuda.set_device(local)
         dist.init_process_group('cpu:gloo,cuda:nccl' if rccl else 'gloo')
         args.device = local % max(1, ndev)
-        if args.comb and args.comb_3d:
-            print("ERROR: a sharded decode runs the 2D comb (NTSC) or the PAL Y/C decoder only")
+        if args.comb and args.comb_3d_flow:
+            print("ERROR: a sharded decode runs the 2D / 3D (-F) comb (NTSC) or the PAL Y/C decoder: the optical "
+                  "flow's estimate chains over every frame")
             return 1
     dec = GPUDecoder(system=system, device=args.device, batch=args.batch)
     if args.comb_args:
@@ -207,8 +208,8 @@ def main(argv=None):
 
     num_frames = req_frames if req_frames is not None else infile_size // bytes_per_frame - firstframe
     if world > 1 or args.epoch_frames or args.manifest:
-        if args.comb and args.comb_3d:
-            print("ERROR: a sharded or epoch-wise decode runs the 2D comb (NTSC) or the PAL Y/C decoder only")
+        if args.comb and args.comb_3d and (args.epoch_frames or args.manifest):
+            print("ERROR: an epoch-wise decode runs the 2D comb (NTSC) or the PAL Y/C decoder only")
             return 1
         if dec.ctx.comb_width != 744:
             print("ERROR: a sharded or epoch-wise decode does not hand comb-ntsc -W's Y-NR history across pieces")
@@ -365,7 +366,8 @@ def sharded(args, dec, outname, firstframe, num_frames, nextsample, req_frames, 
     complete decode: the next starts from the exact chain state after its last frame
     (ShardedDecode.end_state), so the result equals one decode; with --manifest the
     state is saved after every epoch and a rerun resumes after the last finished one."""
-    from ldgpu.shard import decode_sharded
+    from ldgpu.shard import comb3d_sharded, decode_sharded
+    comb3d = bool(args.comb and args.comb_3d)      # after the decode, on the rank's frames
     if world > 1:
         import torch.distributed as dist
         rank = dist.get_rank()
@@ -449,7 +451,8 @@ def sharded(args, dec, outname, firstframe, num_frames, nextsample, req_frames, 
         # (bounded host memory for any capture length)
         res = decode_sharded(dec, rank, world, allgather, start_frame=firstframe, length=n,
                              start_sample=man['nextsample'], whole_capture=whole,
-                             spill_dir=os.path.dirname(os.path.abspath(outname)), comb=args.comb, stats=stats,
+                             spill_dir=os.path.dirname(os.path.abspath(outname)), comb=args.comb and not comb3d,
+                             stats=stats,
                              init=man['state'], epoch_end=ep, widen=widen)
         sizes = allgather((len(res), sum(r[2].nbytes for r in res)))
         first = man['frames'] + sum(k for k, _ in sizes[:rank])
@@ -464,7 +467,19 @@ def sharded(args, dec, outname, firstframe, num_frames, nextsample, req_frames, 
             for fh in (tbc, pcm):         # on storage before the manifest claims the epoch
                 fh.flush()
                 os.fsync(fh.fileno())
-        if args.comb:
+        if comb3d:
+            # the 3D comb (-d 3 -F) over the rank's frames with its neighbours' boundary
+            # frames and the exact burst-level EMA (ldgpu/shard.py comb3d_sharded); output
+            # index = global frame - 1 (the capture's first and last frames have no rgb48)
+            outs = comb3d_sharded(dec, rank, allgather, [r[1] for r in res], first, args.comb_3d_core,
+                                  args.comb_3d_range, stats)
+            with open(outname + '.rgb', 'r+b') as fh:
+                for k, rgb in outs:
+                    fh.seek(k * rgb_bytes)
+                    fh.write(np.ascontiguousarray(rgb).tobytes())
+                fh.flush()
+                os.fsync(fh.fileno())
+        elif args.comb:
             # combed in HBM during the decode; the burst-level EMA (comb-ntsc.cxx:560-566,
             # global over every frame) was handed across the ranks and the first frames
             # re-combed with it (ldgpu/shard.py comb_fix)

@@ -503,6 +503,52 @@ def comb_fix(sd, allgather, nkept, stats=None):
     return a0
 
 
+def comb3d_sharded(dec, rank, allgather, frames, base, core_ire=-1.0, range_ire=-1.0, stats=None):
+    """The 3D comb without optical flow (comb-ntsc -d 3 -F, comb-ntsc.cxx:369-412,834-892)
+    over one sharded decode's frames: every rank combs its own frames.  The single process
+    combs frame g with frames g - 1 and g + 1 once g + 1 has arrived, every frame but the
+    capture's first and last, with the burst-level EMA chained over those frames in order
+    (ToRGB :560-566).  Here each rank receives the frames just outside its range (the
+    previous rank's last, the next rank's first: one frame each way), takes the exact EMA
+    entering its first combed frame from the earlier ranks' chain summaries (as the 2D
+    comb_fix), and runs the device 3D comb over [prev] + its frames + [next]: the rgb48 of
+    every frame it holds that has both neighbours, exactly the single process's.
+    frames: this rank's decoded frames in order (global indices base, base + 1, ...).
+    Returns [(output index, rgb48)], output index = global frame index - 1 (the single
+    process's .rgb holds frames 1 .. N - 2).  Collective: every rank calls it."""
+    n = len(frames)
+    info = allgather({'n': n, 'base': base,
+                      'first': np.array(frames[0]) if n else None, 'last': np.array(frames[-1]) if n else None})
+    total = sum(i['n'] for i in info)
+    prev = next((i['last'] for i in reversed(info[:rank]) if i['n']), None)
+    nxt = next((i['first'] for i in info[rank + 1:] if i['n']), None)
+    # the frames this rank combs (both neighbours in the capture), and the EMA entering them
+    lo, hi = max(base, 1), min(base + n, total - 1)          # global [lo, hi)
+    line0 = 20 if dec.ctx.comb_lines == 525 else COMB_LINE0
+    levels = comb_burst_levels(frames[lo - base:hi - base] if hi > lo else [], line0=line0)
+    summ = allgather(comb_summary(levels))
+    a0 = comb_start_from_summaries(summ, rank, -1.0)
+    if any(comb_start_from_summaries(summ, r, -1.0) is None for r in range(len(summ))):
+        a0 = comb_start_state(allgather(levels), rank, -1.0)   # a chain without a burst for too long
+    out = []
+    if n:
+        dec.ctx.comb_reset()
+        dec.ctx.comb_set_state(a0)
+        g = lo                                       # the next output's global frame index
+        window = ([prev] if prev is not None else []) + [frames[i] for i in range(n)] + \
+            ([nxt] if nxt is not None else [])
+        step = max(1, dec.ctx.max_frames)
+        for i in range(0, len(window), step):
+            for rgb in dec.ctx.comb_ntsc3d(np.stack([np.asarray(f) for f in window[i:i + step]]), core_ire,
+                                           range_ire):
+                out.append((g - 1, rgb))
+                g += 1
+        assert g == max(hi, lo), (g, lo, hi)
+    if stats is not None:
+        stats['comb3d_frames'] = stats.get('comb3d_frames', 0) + len(out)
+    return out
+
+
 def decode_sharded(dec, rank, world, allgather, sink=None, start_frame=0, length=None, start_sample=None,
                    whole_capture=None, spill_dir=None, resident=False, comb=False, stats=None, init=None,
                    epoch_end=None, widen=None):

@@ -220,6 +220,36 @@ def test_cli_sharded_two_ranks_equal_single(tmp_path):
 
 
 @pytest.mark.gpu
+def test_cli_sharded_comb_3d_equals_single(tmp_path):
+    """The 3D comb (comb-ntsc -d 3 -F: --comb --comb-3d) on a sharded decode: 2 and 3 ranks
+    (each combing its own frames with its neighbours' boundary frames and the exact
+    burst-level EMA, ldgpu/shard.py comb3d_sharded) write the same .rgb -- every frame
+    but the capture's first and last -- as one process, byte for byte."""
+    import socket
+    from ldgpu.synth import make_capture
+    data = make_capture(int(40e6 * 0.6), 'u8', first_frame=700, seed=19)
+    cap = tmp_path / 'cap.u8'
+    cap.write_bytes(bytes(data))
+    r = run_cli('--comb', '--comb-3d', cap, tmp_path / 'one')
+    assert r.returncode == 0, r.stderr[-2000:]
+    one = (tmp_path / 'one.rgb').read_bytes()
+    nfr = len((tmp_path / 'one.tbc').read_bytes()) // 955500
+    assert nfr >= 8 and len(one) == (nfr - 2) * 744 * 480 * 3 * 2
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY='0')
+    for n in (2, 3):
+        with socket.socket() as sk:
+            sk.bind(('127.0.0.1', 0))
+            port = sk.getsockname()[1]
+        out = tmp_path / ('r%d' % n)
+        r = subprocess.run([sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', '--nproc-per-node', str(n),
+                            '--master-addr', '127.0.0.1', '--master-port', str(port), CLI, '--comb', '--comb-3d',
+                            str(cap), str(out)], capture_output=True, text=True, timeout=600, env=env)
+        assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-3000:])
+        assert (tmp_path / ('r%d.rgb' % n)).read_bytes() == one, n
+        assert (tmp_path / ('r%d.tbc' % n)).read_bytes() == (tmp_path / 'one.tbc').read_bytes()
+
+
+@pytest.mark.gpu
 def test_cli_sharded_pal_equal_single(tmp_path):
     """PAL sharded too: 3 ranks on a PAL CLV capture write the same .tbc /
     .pcm / .json and, with --comb, the same PAL Y/C .rgb as one process (the Y/C decoder's

@@ -537,3 +537,75 @@ def test_comb_summaries_give_the_exact_start_state():
             assert ex == sp
         ex, sp = comb_chain(ex, part), comb_chain(sp, part)
     assert comb_redo_frames(-1.0, lv[2], 487) == 0
+
+
+class _FakeComb3D:
+    """comb_ntsc3d's contract on a host (no GPU): history of the last two inputs, one output
+    per frame with both neighbours, the burst-level EMA chained over the outputs' frames.
+    An output is (the frame's label, the EMA entering it, its two neighbours' labels)."""
+    comb_lines, max_frames = 480, 3
+
+    def __init__(self):
+        self.hist, self.state = [], -1.0
+
+    def comb_reset(self):
+        self.hist, self.state = [], -1.0
+
+    def comb_set_state(self, a):
+        self.state = float(a)
+
+    def comb_ntsc3d(self, frames, core, rng):
+        from ldgpu.shard import comb_burst_levels, comb_chain
+        out = []
+        for f in frames:
+            self.hist = (self.hist + [np.asarray(f)])[-3:]
+            if len(self.hist) == 3:
+                p, c, n = self.hist
+                out.append(np.array([c[0], self.state, p[0], n[0]], dtype=np.float64))
+                self.state = comb_chain(self.state, comb_burst_levels([c]))
+        return out
+
+
+def test_comb3d_sharded_equals_one_process_over_any_split():
+    """ldgpu/shard.py comb3d_sharded: the ranks' 3D-comb outputs, put together by their
+    output index, are the single process's -- every frame but the first and last, each
+    with its true neighbours and the exact burst-level EMA (ranks with no frames too)."""
+    import threading
+    from ldgpu.shard import comb3d_sharded
+    rng = np.random.default_rng(5)
+    N = 11
+    frames = []
+    for g in range(N):
+        f = np.zeros(525 * 910, dtype=np.uint16)
+        f[0] = 1000 + g                                          # the frame's label
+        lv = rng.integers(0, 4000, 525)
+        lv[rng.random(525) < 0.3] = 0                            # lines without burst
+        f[np.arange(525) * 910 + 1] = lv
+        frames.append(f)
+
+    class Dec:
+        def __init__(self):
+            self.ctx = _FakeComb3D()
+    one = Dec()
+    want = [(i, o) for i, o in enumerate(one.ctx.comb_ntsc3d(frames, -1, -1))]
+    for split in ([0, 4, 7, 11], [0, 1, 2, 11], [0, 5, 5, 11], [0, 11, 11, 11], [0, 3, 10, 11]):
+        world = len(split) - 1
+        bar = threading.Barrier(world)
+        slots = [None] * world
+        got = [None] * world
+
+        def run(r):
+            def ag(obj):
+                slots[r] = obj
+                bar.wait()
+                res = list(slots)
+                bar.wait()
+                return res
+            got[r] = comb3d_sharded(Dec(), r, ag, frames[split[r]:split[r + 1]], split[r])
+        th = [threading.Thread(target=run, args=(r,)) for r in range(world)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+        allout = sorted((k, tuple(o)) for part in got for k, o in part)
+        assert allout == [(k, tuple(o)) for k, o in want], split
