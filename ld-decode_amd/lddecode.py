@@ -220,6 +220,9 @@ def main(argv=None):
     rgb = open(outname + '.rgb', 'wb') if args.comb else None
     meta_all = []
     w = Writer()
+    # the .rgb (2.2 MB per frame, more than twice the .tbc) on a writer of its own: the
+    # two files' writes proceed in parallel (a file's buffered writes are serialised)
+    w_rgb = Writer() if rgb else None
 
     def sink(frame, audio, meta):
         def write():
@@ -230,23 +233,29 @@ def main(argv=None):
         w.put(write)
 
     def comb_sink(r):
-        w.put(lambda: rgb.write(np.ascontiguousarray(r)))
+        w_rgb.put(lambda: rgb.write(np.ascontiguousarray(r)))
 
     def frame_log(lines):
         w.put(lambda: print('\n'.join(lines)))   # the reference's per-field lines
 
+    def drain():
+        w.drain()
+        if w_rgb:
+            w_rgb.drain()
+
     dec.frame_log = frame_log
-    dec.before_ring_reuse = w.drain
+    dec.before_ring_reuse = drain
     t0 = time.perf_counter()
     try:
         n = dec.decode(start_frame=firstframe, length=num_frames, sink=sink, comb=args.comb,
                        comb_sink=comb_sink if rgb else None, start_sample=nextsample,
                        comb3d=(args.comb_3d_core, args.comb_3d_range) if args.comb_3d else None)
         t_dec = time.perf_counter() - t0
-        w.close()
     finally:
         dec.before_ring_reuse = None
         w.close()
+        if w_rgb:
+            w_rgb.close()
     if req_frames is not None and n < req_frames:
         print('Warning: end of file reached before requested number of frames were decoded')
     tbc.close()
@@ -258,11 +267,11 @@ def main(argv=None):
             json.dump(meta_all, fh)
     t_all = time.perf_counter() - t0
     if args.stats_json:
-        write_stats(args.stats_json, dec, n, meta_all, t_dec, t_all, w)
+        write_stats(args.stats_json, dec, n, meta_all, t_dec, t_all, w, w_rgb)
     return 0
 
 
-def write_stats(path, dec, n, metas, t_dec, t_all, w):
+def write_stats(path, dec, n, metas, t_dec, t_all, w, w_rgb=None):
     """The run's timing breakdown (one process): where the wall time went between
     reading the file, the decode, and writing the outputs."""
     first = metas[0]['fields'][0]['readsample'] if metas else 0
@@ -275,6 +284,8 @@ def write_stats(path, dec, n, metas, t_dec, t_all, w):
            'decode_thread_s': {k: round(st.get(k, 0.0), 4) for k in ('plan_s', 'gpu_s', 'replay_s', 'flush_s',
                                                                        'wait_s')},
            'writer': {'busy_s': round(w.busy_s, 4), 'decode_waited_s': round(w.drain_s, 4)},
+           'rgb_writer': ({'busy_s': round(w_rgb.busy_s, 4), 'decode_waited_s': round(w_rgb.drain_s, 4)}
+                          if w_rgb else None),
            'reads_decoded': st.get('reads'), 'reads_used': st.get('reads_used'),
            'stream_seeks': st.get('stream_seeks', 0)}
     if dec.stream:
