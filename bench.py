@@ -92,6 +92,10 @@ def parse():
                     help='PCIe-inclusive (not the headline): each step hands the capture over from host memory '
                          '(ldg_set_capture) and returns the .tbc frames, audio and rgb48 to host buffers, '
                          "as lddecode.py's file path does minus the disk (u8 only)")
+    ap.add_argument('--stream-file', default=None,
+                    help='not the headline: the capture is written to this file once, and each step streams it '
+                         'from there through the HBM ring (ldg_stream_open, 2 GiB; lddecode.py\'s path minus the '
+                         'output writes), frames and rgb48 left in HBM')
     ap.add_argument('--prof-all', action='store_true',
                     help='HIP-event timing of every kernel (default: the demod only, the roofline kernel)')
     return ap.parse_args()
@@ -113,6 +117,11 @@ def _oracle_decode(data, fmt=0, system='NTSC', frames=None):
 
 
 SLICE_SHIFT = 170004          # about a quarter field of 40 MSPS RF (a multiple of 12: whole packing groups)
+
+
+def bytes_for_samples_(fmt, n):
+    from ldgpu.formats import bytes_for_samples
+    return bytes_for_samples(fmt, n)
 
 
 def _sample_bytes(fmt, n):
@@ -267,7 +276,7 @@ class CaptureWorkload:
     (CAV by default) synthesised straight into HBM.  Weak scaling, no data-path collective."""
 
     def __init__(self, args, dec, rank):
-        self.args, self.dec = args, dec
+        self.args, self.dec, self.rank = args, dec, rank
         self.nsamp = int(40e6 * (args.seconds or 60.0))
         t0 = time.perf_counter()
         # per-rank capture: its own CAV picture-number range and noise seed
@@ -276,6 +285,12 @@ class CaptureWorkload:
         dec.use_resident_capture(args.fmt, self.nsamp)
         self.synth_s = time.perf_counter() - t0
         self.host_cap = None
+        self.stream_acc = {}
+        if args.stream_file:
+            nbytes = bytes_for_samples_(args.fmt, self.nsamp)
+            with open(args.stream_file, 'wb') as fh:
+                for off in range(0, nbytes, 1 << 28):
+                    fh.write(dec.ctx.capture_download(off, min(1 << 28, nbytes - off)))
         if args.host_io:
             if args.fmt != 0:
                 raise SystemExit('--host-io: u8 captures only')
@@ -286,6 +301,17 @@ class CaptureWorkload:
 
     def step(self):
         dec, args = self.dec, self.args
+        if args.stream_file:
+            t0 = time.perf_counter()
+            dec.open_stream(args.stream_file, args.fmt, 2 << 30)      # the file read inside the step
+            t1 = time.perf_counter()
+            n = dec.decode(sink=None, comb=not args.no_comb)
+            st = dec.ctx.stream_stats()
+            acc = self.stream_acc
+            acc['open_s'] = acc.get('open_s', 0.0) + t1 - t0
+            for k in ('read_s', 'launch_wait_s', 'space_wait_s', 'stage_wait_s', 'bytes_read', 'launch_waits'):
+                acc[k] = acc.get(k, 0.0) + st[k]
+            return n, dec.last_meta['nextsample']
         if self.host_cap is not None:
             dec.set_capture(self.host_cap, args.fmt)         # H2D of the whole capture inside the step
             n = dec.decode(sink=lambda fr, au, meta: None, comb=not args.no_comb, comb_sink=lambda rgb: None)
@@ -297,8 +323,20 @@ class CaptureWorkload:
     def host_capture(self, nbytes):
         from ldgpu.formats import bytes_for_samples
         nbytes = min(nbytes, bytes_for_samples(self.fmt, self.nsamp))
+        if self.args.stream_file:
+            return np.fromfile(self.args.stream_file, dtype=np.uint8, count=nbytes)
         return self.host_cap[:nbytes] if self.host_cap is not None else \
             np.asarray(self.dec.ctx.capture_download(0, nbytes))
+
+    def before_iso(self):
+        """The roofline leg re-demodulates cached reads from a resident capture: after
+        streamed steps, the capture is made resident again and a few frames decoded."""
+        if self.args.stream_file:
+            a = self.args
+            self.dec.ctx.synth(self.nsamp, fmt=a.fmt, first_frame=1 + 2000 * (self.rank % 39), clv=a.clv,
+                               seed=20181015 + self.rank)
+            self.dec.use_resident_capture(a.fmt, self.nsamp)
+            self.dec.decode(sink=None, comb=False, length=120)
 
     def config(self, frames):
         a = self.args
@@ -307,12 +345,17 @@ class CaptureWorkload:
                                '' if a.no_comb else '->2D comb rgb48'),
                 'frames_per_step': frames // max(a.steps, 1), 'batch_reads': a.batch,
                 'parallelism': 'capture-sharded x%d' % int(os.environ.get('WORLD_SIZE', '1')),
-                'io': 'host buffers over PCIe (--host-io)' if a.host_io else 'HBM-resident'}
+                'io': ('host buffers over PCIe (--host-io)' if a.host_io else
+                       'streamed from a file through a 2 GiB HBM ring (--stream-file)' if a.stream_file else
+                       'HBM-resident')}
 
     def checks(self):
         nrs = self.dec.frame_numbers       # consecutive picture numbers, all frames present
         ok = all(b == a + 1 for a, b in zip(nrs, nrs[1:]))
-        return {'framenr_consecutive': ok, 'cav_framenr_consecutive': ok}   # (the round-1 key, kept)
+        out = {'framenr_consecutive': ok, 'cav_framenr_consecutive': ok}   # (the round-1 key, kept)
+        if self.stream_acc:
+            out['stream'] = {k: round(v, 4) for k, v in self.stream_acc.items()}
+        return out
 
 
 class ShardedWorkload:
@@ -571,6 +614,8 @@ def main():
     # the roofline leg: the demod alone (kernel ldg_k_demod_iso) over one full-width launch's
     # reads, ISO_ITERS launches back to back, HIP events on its stream -- the per-dispatch
     # figure a kernel trace of this command reports for ldg_k_demod_iso (profiles/)
+    if hasattr(wl, 'before_iso'):
+        wl.before_iso()
     if dist is not None and shared_device:
         # ranks sharing a GPU (a rehearsal on a smaller box) take the leg in turn, so each
         # times the kernel alone on the device as a one-rank-per-GPU run does

@@ -176,7 +176,10 @@ int ldg_set_capture(ldg_ctx* ctx, const void* data, int64_t nsamples, int fmt, i
  *     finished.  A launch whose reads end past the ring's reach (ldg_stream_window
  *     out[1]) fails with LDG_ESTATE; reads starting below the released point come back
  *     LDG_FS_EOF.
- * ldg_stream_seek restarts the stream at another sample (no decode outstanding).
+ * ldg_stream_seek restarts the stream at another sample (no decode outstanding).  Opening
+ * a file while a stream of the same ring_bytes is open reuses its ring (no decode
+ * outstanding).  The chunks' copies rotate over four copy streams (LDG_STREAM_COPIES
+ * sets 1 - 4), one host-to-device DMA engine each.
  * ldg_set_capture, ldg_synth_capture and ldg_destroy close the stream. */
 int ldg_stream_open(ldg_ctx* ctx, const char* path, int fmt, int64_t ring_bytes, int64_t first_sample);
 int ldg_stream_release(ldg_ctx* ctx, int64_t below_sample);
@@ -186,7 +189,7 @@ int ldg_stream_seek(ldg_ctx* ctx, int64_t first_sample);
 int ldg_stream_window(ldg_ctx* ctx, int64_t* out4);
 /* Up to n doubles: bytes read, seconds in read(2), chunks, launches that waited for data,
  * seconds they waited, seconds the reader waited for ring space, seeks, ring bytes, chunk
- * bytes.  Returns the count written. */
+ * bytes, seconds the reader waited for a staging buffer's copy.  Returns the count written. */
 int ldg_stream_stats(ldg_ctx* ctx, double* out, int n);
 int ldg_stream_close(ldg_ctx* ctx);
 

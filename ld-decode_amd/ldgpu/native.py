@@ -31,7 +31,7 @@ EXPORTS = ['ldg_create', 'ldg_destroy', 'ldg_last_error', 'ldg_set_filters', 'ld
            'ldg_stream_open', 'ldg_stream_release', 'ldg_stream_seek', 'ldg_stream_window', 'ldg_stream_stats',
            'ldg_stream_close', 'ldg_device_memory']
 STREAM_STATS = ('bytes_read', 'read_s', 'chunks', 'launch_waits', 'launch_wait_s', 'space_wait_s', 'seeks',
-                'ring_bytes', 'chunk_bytes')     # ldg_stream_stats, in order
+                'ring_bytes', 'chunk_bytes', 'stage_wait_s')     # ldg_stream_stats, in order
 
 
 class FieldInfo(C.Structure):
