@@ -120,6 +120,42 @@ def test_stream_decode_equals_resident(case, ring_mb, tmp_path):
     dec.ctx.close()
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize('copies', ['1', '3'])
+def test_stream_copy_streams_and_ring_reuse(copies, tmp_path, monkeypatch):
+    """The chunks' copies rotate over LDG_STREAM_COPIES streams (default 4): with 1 and 3
+    (a count that does not divide the ring's chunks) the decode through a 2 MiB ring is the
+    resident one; a second file opened at the same ring size reuses the ring (no new
+    device memory) and decodes to its own golden output."""
+    sys.path.insert(0, os.path.join(HERE, 'golden'))
+    import make_golden
+    from ldgpu.decoder import GPUDecoder
+    from ldgpu.native import device_memory
+    monkeypatch.setenv('LDG_STREAM_COPIES', copies)
+    dec = GPUDecoder(system='NTSC', batch=16)
+    for i, case in enumerate(('ntsc_cav_u8_0p2s', 'ntsc_cav_u8_mid_0p2s')):
+        with open(os.path.join(HERE, 'golden', case + '.json')) as fh:
+            gold = json.load(fh)
+        data = make_golden.build_capture(case)
+        path = tmp_path / ('cap%d.u8' % i)
+        path.write_bytes(bytes(data))
+        free0 = device_memory(0)[0]
+        dec.open_stream(str(path), 0, 2 << 20)
+        if i:
+            assert abs(device_memory(0)[0] - free0) < 1 << 20     # the same ring, reused
+        got = _decode(dec)
+        assert len(got) == len(gold['frames'])
+        for (f1, a1, m1), g in zip(got, gold['frames']):
+            assert m1 == g['meta']
+            assert hashlib.sha256(a1.tobytes()).hexdigest() == g['pcm_sha256']
+        if i == 0:
+            dec.set_capture(data, 0)
+            want = _decode(dec)
+            assert all(np.array_equal(a[0], b[0]) for a, b in zip(got, want))
+            dec.open_stream(str(path), 0, 2 << 20)      # (set_capture closed the stream)
+    dec.ctx.close()
+
+
 def _run_cli(*args):
     return subprocess.run([sys.executable, CLI, *map(str, args)], capture_output=True, text=True, timeout=600)
 
