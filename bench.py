@@ -560,6 +560,10 @@ def main():
         local = local % max(ndev, 1)
         torch.cuda.set_device(local)
         tdist.init_process_group('nccl' if use_nccl else 'gloo')
+        if use_nccl:
+            # the RCCL communicator made by a collective every rank joins, before the halo's
+            # batched send / receive (which only neighbouring ranks join)
+            tdist.all_reduce(torch.zeros(1, device='cuda'))
         dist = tdist
 
     from ldgpu.decoder import GPUDecoder

@@ -154,6 +154,11 @@ def main(argv=None):
         if rccl:
             torch.cuda.set_device(local)
         dist.init_process_group('cpu:gloo,cuda:nccl' if rccl else 'gloo')
+        if rccl:
+            # the RCCL communicator made by a collective every rank joins: the first device
+            # operation after this is the halo's batched send / receive, which only
+            # neighbouring ranks join (torch requires every rank in a first batched P2P call)
+            dist.all_reduce(torch.zeros(1, device='cuda'))
         args.device = local % max(1, ndev)
         if args.comb and args.comb_3d_flow:
             print("ERROR: a sharded decode runs the 2D / 3D (-F) comb (NTSC) or the PAL Y/C decoder: the optical "
