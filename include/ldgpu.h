@@ -176,9 +176,9 @@ int ldg_set_capture(ldg_ctx* ctx, const void* data, int64_t nsamples, int fmt, i
  *     finished.  A launch whose reads end past the ring's reach (ldg_stream_window
  *     out[1]) fails with LDG_ESTATE; reads starting below the released point come back
  *     LDG_FS_EOF.
- * ldg_stream_seek restarts the stream at another sample.  Opening a file while a stream
- * of the same ring_bytes is open reuses its ring.  Both need no decode outstanding
- * (LDG_ESTATE otherwise).  The chunks' copies rotate over four copy streams (LDG_STREAM_COPIES
+ * ldg_stream_seek restarts the stream at another sample (no decode outstanding).  Opening
+ * a file while a stream of the same ring_bytes is open reuses its ring (no decode
+ * outstanding).  The chunks' copies rotate over four copy streams (LDG_STREAM_COPIES
  * sets 1 - 4), one host-to-device DMA engine each.
  * ldg_set_capture, ldg_synth_capture and ldg_destroy close the stream. */
 int ldg_stream_open(ldg_ctx* ctx, const char* path, int fmt, int64_t ring_bytes, int64_t first_sample);
