@@ -156,6 +156,38 @@ def test_stream_copy_streams_and_ring_reuse(copies, tmp_path, monkeypatch):
     dec.ctx.close()
 
 
+@pytest.mark.gpu
+def test_stream_edge_files(tmp_path):
+    """A missing file fails loudly at the open; a file shorter than two frames is refused
+    by the decode exactly as the resident capture is ('start frame is past end of file',
+    lddecode.py:49 with the 10-bit frame size); the stream then still decodes a good file."""
+    sys.path.insert(0, os.path.join(HERE, 'golden'))
+    import make_golden
+    from ldgpu.decoder import GPUDecoder
+    from ldgpu.native import LDGError
+    dec = GPUDecoder(system='NTSC', batch=16)
+    with pytest.raises(LDGError, match='cannot open'):
+        dec.open_stream(str(tmp_path / 'missing.u8'), 0, 2 << 20)
+    short = bytes(make_golden.build_capture('ntsc_cav_u8_0p2s'))[:1000000]
+    path = tmp_path / 'short.u8'
+    path.write_bytes(short)
+    errs = []
+    for opener in (lambda: dec.set_capture(short, 0), lambda: dec.open_stream(str(path), 0, 2 << 20)):
+        opener()
+        with pytest.raises(ValueError) as e:
+            dec.decode(sink=lambda *a: None)
+        errs.append(str(e.value))
+    assert errs[0] == errs[1] == 'start frame is past end of file'
+    with open(os.path.join(HERE, 'golden', 'ntsc_cav_u8_0p2s.json')) as fh:
+        gold = json.load(fh)
+    good = tmp_path / 'good.u8'
+    good.write_bytes(bytes(make_golden.build_capture('ntsc_cav_u8_0p2s')))
+    dec.open_stream(str(good), 0, 2 << 20)
+    got = _decode(dec)
+    assert [m for _, _, m in got] == [g['meta'] for g in gold['frames']]
+    dec.ctx.close()
+
+
 def _run_cli(*args):
     return subprocess.run([sys.executable, CLI, *map(str, args)], capture_output=True, text=True, timeout=600)
 
