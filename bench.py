@@ -757,6 +757,10 @@ def main():
                        reads_used=dec.stats['reads_used'], batches=dec.stats['batches'],
                        misses=dec.stats.get('misses', 0), drain_waits=dec.stats.get('drain_waits', 0), vcut_redo=dec.stats.get('vcut_redo', 0), step_ms=step_ms,
                        park_redo=dec.stats.get('migrated', 0),
+                       # SURVEY §8(d)'s protocol reports the median step: rank 0's, beside the mean
+                       step_ms_median=round(float(np.median(step_ms)), 3) if step_ms else None,
+                       value_at_median_step=(round(msps * (dt_max / args.steps * 1e3) / float(np.median(step_ms)), 3)
+                                             if step_ms else None),
                        host_s={k: round(dec.stats.get(k, 0.0), 4)
                                for k in ('plan_s', 'gpu_s', 'replay_s', 'flush_s', 'wait_s')},
                        inflight_at_wait=dec.stats.get('inflight_at_wait'), demod_issue=issue),
