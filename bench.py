@@ -95,10 +95,14 @@ def parse():
     ap.add_argument('--stream-file', default=None,
                     help='not the headline: the capture is written to this file once, and each step streams it '
                          'from there through the HBM ring (ldg_stream_open, 2 GiB; lddecode.py\'s path minus the '
-                         'output writes), frames and rgb48 left in HBM')
+                         'output writes), frames and rgb48 left in HBM; NTSC, one rank or --independent')
     ap.add_argument('--prof-all', action='store_true',
                     help='HIP-event timing of every kernel (default: the demod only, the roofline kernel)')
-    return ap.parse_args()
+    args = ap.parse_args()
+    world = int(os.environ.get('WORLD_SIZE', '1'))
+    if (args.stream_file or args.host_io) and (args.system == 'PAL' or (world > 1 and not args.independent)):
+        ap.error('--stream-file / --host-io: the NTSC capture workload (one rank, or --independent)')
+    return args
 
 
 def _oracle_decode(data, fmt=0, system='NTSC', frames=None):
@@ -286,9 +290,13 @@ class CaptureWorkload:
         self.synth_s = time.perf_counter() - t0
         self.host_cap = None
         self.stream_acc = {}
+        # --stream-file: each rank streams its own file (--independent N > 1: path.<rank>)
+        self.stream_path = None
         if args.stream_file:
+            world = int(os.environ.get('WORLD_SIZE', '1'))
+            self.stream_path = args.stream_file if world == 1 else '%s.%d' % (args.stream_file, rank)
             nbytes = bytes_for_samples_(args.fmt, self.nsamp)
-            with open(args.stream_file, 'wb') as fh:
+            with open(self.stream_path, 'wb') as fh:
                 for off in range(0, nbytes, 1 << 28):
                     fh.write(dec.ctx.capture_download(off, min(1 << 28, nbytes - off)))
         if args.host_io:
@@ -303,7 +311,7 @@ class CaptureWorkload:
         dec, args = self.dec, self.args
         if args.stream_file:
             t0 = time.perf_counter()
-            dec.open_stream(args.stream_file, args.fmt, 2 << 30)      # the file read inside the step
+            dec.open_stream(self.stream_path, args.fmt, 2 << 30)      # the file read inside the step
             t1 = time.perf_counter()
             n = dec.decode(sink=None, comb=not args.no_comb)
             st = dec.ctx.stream_stats()
@@ -323,8 +331,8 @@ class CaptureWorkload:
     def host_capture(self, nbytes):
         from ldgpu.formats import bytes_for_samples
         nbytes = min(nbytes, bytes_for_samples(self.fmt, self.nsamp))
-        if self.args.stream_file:
-            return np.fromfile(self.args.stream_file, dtype=np.uint8, count=nbytes)
+        if self.stream_path:
+            return np.fromfile(self.stream_path, dtype=np.uint8, count=nbytes)
         return self.host_cap[:nbytes] if self.host_cap is not None else \
             np.asarray(self.dec.ctx.capture_download(0, nbytes))
 
