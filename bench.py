@@ -100,7 +100,8 @@ def parse():
                     help='HIP-event timing of every kernel (default: the demod only, the roofline kernel)')
     args = ap.parse_args()
     world = int(os.environ.get('WORLD_SIZE', '1'))
-    if (args.stream_file or args.host_io) and (args.system == 'PAL' or (world > 1 and not args.independent)):
+    if (args.stream_file or args.host_io) and (args.system == 'PAL' or args.sharded or
+                                               (world > 1 and not args.independent)):
         ap.error('--stream-file / --host-io: the NTSC capture workload (one rank, or --independent)')
     return args
 
