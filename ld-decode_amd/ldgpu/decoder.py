@@ -183,12 +183,23 @@ def field_log_lines(fields, ntsc):
 
 
 class FrameOut:
-    __slots__ = ('top', 'bottom', 'audio_fields', 'vbi', 'nextsample', 'fields', 'index', 'start', 'tstart', 'mtf0',
-                 'log', 'end')
+    __slots__ = ('top', 'bottom', 'audio_fields', 'vbi', 'nextsample', 'field_objs', '_fields', 'index', 'start',
+                 'tstart', 'mtf0', 'log', 'end')
 
     def __init__(self, **kw):
+        self._fields = None
         for k, v in kw.items():
             setattr(self, k, v)
+
+    @property
+    def fields(self):
+        """The metadata records of the fields this frame's readframe read (GPUField.record),
+        built on first use: the replay only keeps the fields (a field's record does not
+        change once its frame is complete), so a decode whose per-frame metadata nobody
+        reads (the benchmark's sink=None) does not build them on its critical path."""
+        if self._fields is None:
+            self._fields = [x.record() for x in self.field_objs]
+        return self._fields
 
 
 class GPUDecoder:
@@ -1077,7 +1088,7 @@ class GPUDecoder:
                 nextsample = fr.nextsample
                 if keep_from is not None and fr.start < keep_from:
                     continue                    # warm-up frame: chains only
-                fr.fields = [x.record() for x in self.field_log]
+                fr.field_objs = self.field_log
                 fr.log = field_log_lines(self.field_log, self.sysp.name == 'NTSC') if self.frame_log else None
                 fr.index = done + len(frames)
                 frames.append(fr)
@@ -1101,7 +1112,7 @@ class GPUDecoder:
             if self.htrace is not None:
                 self.htrace.append((time.perf_counter(), 'flushed', len(frames)))
             done += len(frames)
-            self.stats['reads_used'] += sum(len(f.fields) for f in frames)
+            self.stats['reads_used'] += sum(len(f.field_objs) for f in frames)
             if window_miss is not None:
                 raise window_miss
             if eof or (not frames and not launched and not self.pending):
@@ -1219,14 +1230,18 @@ class GPUDecoder:
             if counts[j] < 0:
                 raise ReferenceCrash('audio index error (reference: field invalid)')
             per_frame[fr_i].append(pcm[j, :2 * counts[j]])
+        def meta_of(fr):
+            return {'frame': fr.index, 'vbi': dict(fr.vbi), 'nextsample': int(fr.nextsample), 'fields': fr.fields}
         for i, fr in enumerate(frames):
-            audio = np.concatenate(per_frame[i]) if per_frame[i] else np.zeros(0, dtype=np.int16)
-            meta = {'frame': fr.index, 'vbi': dict(fr.vbi), 'nextsample': int(fr.nextsample), 'fields': fr.fields}
-            self.last_meta = meta
             self.frame_numbers.append(fr.vbi['framenr'])
             if fr.log:
                 self.frame_log(fr.log)
             if sink:
+                audio = np.concatenate(per_frame[i]) if per_frame[i] else np.zeros(0, dtype=np.int16)
+                meta = meta_of(fr)
+                self.last_meta = meta
                 sink(pics[i], audio, meta)
             else:
-                self.pcm_samples += audio.size
+                self.pcm_samples += sum(a.size for a in per_frame[i])
+        if frames and not sink:
+            self.last_meta = meta_of(frames[-1])     # (no sink: only the last frame's metadata is read)
