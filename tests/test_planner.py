@@ -240,3 +240,42 @@ def test_demod_isolated_read_count(monkeypatch):
     assert [len(s) for s in seen[-2:]] == [16, 16]
     with pytest.raises(RuntimeError):
         dec.demod_isolated(3, reads=8)              # the read cache was dropped
+
+
+def test_frame_metadata_with_and_without_a_sink(monkeypatch):
+    """Each frame's metadata lists the fields its readframe read, chained read to read
+    (nextsample of one = readsample of the next); the records are built on first use, and
+    a decode without a sink keeps only the last frame's metadata -- the same dict as the
+    sink run's last one."""
+    monkeypatch.setenv('LDG_PROBE', '0')
+    frames = 200
+    nsamples = int(field_start(2 * frames + 4)) + 2_000_000
+    FakeCtx.nsamples, FakeCtx.jitter = nsamples, False
+    monkeypatch.setattr(native, 'Context', FakeCtx)
+    class HostBuf:                                     # PinnedBuffer without ldg_host_alloc
+        def view(self, count):
+            return np.zeros(count, np.uint16)
+
+        def release_retired(self):
+            pass
+    monkeypatch.setattr(native, 'PinnedBuffer', HostBuf)
+    dec = D.GPUDecoder(system='NTSC', device=0, batch=16)
+    dec.use_resident_capture(0, nsamples)
+    dec.ctx.output_async = lambda tops, bots, tbc, rgb=None: None
+    dec.ctx.output_wait = lambda: None
+    dec.ctx.comb_lines, dec.ctx.comb_width = 480, 744
+    metas = []
+    n = dec.decode(sink=lambda fr, au, meta: metas.append(meta))
+    assert n == len(metas) > 100
+    prev = None
+    for m in metas:
+        assert len(m['fields']) >= 2
+        for f in m['fields']:
+            if prev is not None:
+                assert f['readsample'] == prev['nextsample']
+            prev = f
+        assert m['nextsample'] == m['fields'][-1]['nextsample']
+    last = metas[-1]
+    dec.use_resident_capture(0, nsamples)
+    assert dec.decode(sink=None) == n
+    assert dec.last_meta == last
