@@ -188,6 +188,33 @@ def test_stream_edge_files(tmp_path):
     dec.ctx.close()
 
 
+@pytest.mark.gpu
+def test_stream_open_and_seek_refused_with_decodes_outstanding(tmp_path):
+    """ldg_stream_open / ldg_stream_seek need no decode outstanding (they rewrite the ring a
+    launched demod may still read): LDG_ESTATE while a call is in flight, fine after its
+    wait."""
+    sys.path.insert(0, os.path.join(HERE, 'golden'))
+    import make_golden
+    from ldgpu.decoder import GPUDecoder
+    from ldgpu.native import LDGError
+    data = bytes(make_golden.build_capture('ntsc_cav_u8_0p2s'))
+    path = tmp_path / 'cap.u8'
+    path.write_bytes(data)
+    dec = GPUDecoder(system='NTSC', batch=16)
+    dec.open_stream(str(path), 0, 2 << 20)
+    dec.ctx.decode_reads_async([0], [1.0], [0])
+    with pytest.raises(LDGError, match='outstanding'):
+        dec.ctx.stream_open(str(path), 0, 2 << 20)
+    with pytest.raises(LDGError, match='outstanding'):
+        dec.ctx.stream_seek(0)
+    dec.ctx.decode_reads_wait()
+    dec.open_stream(str(path), 0, 2 << 20)
+    with open(os.path.join(HERE, 'golden', 'ntsc_cav_u8_0p2s.json')) as fh:
+        gold = json.load(fh)
+    assert [m for _, _, m in _decode(dec)] == [g['meta'] for g in gold['frames']]
+    dec.ctx.close()
+
+
 def _run_cli(*args):
     return subprocess.run([sys.executable, CLI, *map(str, args)], capture_output=True, text=True, timeout=600)
 
